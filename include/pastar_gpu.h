@@ -1,0 +1,179 @@
+/*
+ * pastar_gpu.h -- C-ABI of the MI355X PAStar frontier-expansion engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (Gabrielcarvfer/mpi_pastar_msa; paths relative to its root):
+ *
+ *   reference interface                           replaced by
+ *   --------------------------------------------  -----------------------------
+ *   read_fasta_file (read_fasta.cpp:43-56)         pastar_read_fasta
+ *   weightAltschulsRationale2 (WeightedSP.cpp:424) pastar_compute_weights
+ *   HeuristicHPair::init (HeuristicHPair.cpp:47)   pastar_gpu_build_heuristic
+ *   HeuristicHPair::calculate_h (:74-86)           pastar_gpu_h
+ *   PairAlign::getScore (PairAlign.cpp:174-177)    pastar_gpu_pair_table
+ *   Node<N>::getNeigh (Node.cpp:206-248, Node.h:37) pastar_gpu_expand
+ *   Coord<N>::get_id (CoordHash.cpp:191-245)       pastar_gpu_owner
+ *   PAStar<N>::pa_star (PAStar.cpp:627-673,        pastar_gpu_search
+ *     PAStar.h:117) incl. worker_inner,
+ *     OpenList / ClosedList (PriorityList.h:52-82,
+ *     PAStar.cpp:92), check_stop (:480-547)
+ *   ClosedList[id][coord] lookups in the backtrace pastar_gpu_closed_lookup,
+ *     (backtrace.cpp:47-69, PAStarDistributed-      pastar_gpu_alignment
+ *      Backtrace.cpp:19-213)
+ *   MPI rank bootstrap (msa_pastar_main.cpp:56-89) pastar_rccl_unique_id +
+ *                                                  pastar_gpu_create(n_shards,
+ *                                                  shard_rank, rccl_id)
+ *
+ * Conventions: plain C types only; every entry point returns an int status
+ * (0 ok, < 0 error) and never throws; pastar_last_error() describes the last
+ * failure of the calling thread.  The caller owns host buffers, the context
+ * owns device memory.  One context per GPU, driven by one host thread.
+ * A process that has no usable gfx950 device gets PASTAR_ENODEV from
+ * pastar_gpu_create: there is no CPU fallback.
+ */
+#ifndef PASTAR_GPU_H
+#define PASTAR_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PASTAR_MAX_SEQ 16
+#define PASTAR_ABI_VERSION 1
+
+/* status codes */
+#define PASTAR_OK 0
+#define PASTAR_EINVAL (-1)   /* bad argument                          */
+#define PASTAR_ENODEV (-2)   /* no HIP device / kernel launch failure */
+#define PASTAR_ENOMEM (-3)   /* device capacity exhausted             */
+#define PASTAR_EIO (-4)      /* file could not be read                */
+#define PASTAR_ENOTFOUND (-5)
+#define PASTAR_ECOMM (-6)    /* RCCL failure                          */
+#define PASTAR_ESTATE (-7)   /* call out of order                     */
+
+/* Coord hash types, same numbering as the reference's hashType enum
+ * (Coord.h:29): HashFZorder, HashPZorder, HashFSum, HashPSum. */
+#define PASTAR_HASH_FZORDER 0
+#define PASTAR_HASH_PZORDER 1
+#define PASTAR_HASH_FSUM 2
+#define PASTAR_HASH_PSUM 3
+
+/* A search problem.  Mirrors the reference's process-global singletons
+ * Sequences (Sequences.h:15-39), Cost (Cost.h:10-50) and
+ * HeuristicHPair::weightMatrix (HeuristicHPair.h:23). */
+typedef struct pastar_problem {
+    int n;                          /* sequences, 2..16                       */
+    const int *lengths;             /* n residue counts (>= 1 each)           */
+    const char *const *residues;    /* n residue strings (lengths[i] chars)   */
+    const int *weights;             /* P = n(n-1)/2 pair weights, pair order
+                                       (0,1),(0,2)..(n-2,n-1) = (int)weight-
+                                       Matrix[x][y]; NULL: computed on the
+                                       host with pastar_compute_weights       */
+    const int *sub;                 /* 128*128 distance table indexed by the
+                                       residue bytes, or NULL for the
+                                       reference table (Cost.cpp:12-262)      */
+    int gap_open, gap_ext, gap_gap; /* Cost.h:13; all 30 in the reference     */
+    int hash_type, hash_shift;      /* CoordHash owner partition (FZORDER, 12)*/
+} pastar_problem;
+
+/* Node<N> (Node.h:28-49): coordinate, g, f and the parent mask `parenti`. */
+typedef struct pastar_node {
+    uint16_t pos[PASTAR_MAX_SEQ];
+    int32_t g;
+    int32_t f;
+    int32_t parent_mask;
+} pastar_node;
+
+/* Tuning of the device-resident search (all zero = defaults). */
+typedef struct pastar_search_opts {
+    int64_t batch_nodes;      /* target open nodes expanded per step        */
+    int64_t table_slots_log2; /* open+closed hash table capacity (log2)     */
+    int64_t near_capacity;    /* entries of the near (f-window) open pile   */
+    int64_t far_capacity;     /* entries of the far open pile               */
+    int64_t max_steps;        /* safety stop (0 = unlimited)                */
+    int32_t profile;          /* 1: time the expand kernel with HIP events  */
+    int32_t verbose;
+} pastar_search_opts;
+
+typedef struct pastar_result {
+    int64_t score;          /* optimal weighted SP score (goal g)              */
+    int64_t expansions;     /* nodes expanded by this shard, incl. the goal   */
+    int64_t expansions_all; /* summed over shards                             */
+    int64_t reopen;         /* re-expansions with a better g (PAStar Reopen)  */
+    int64_t generated;      /* neighbours produced                            */
+    int64_t open_size;      /* live open entries at termination               */
+    int64_t closed_size;    /* distinct expanded nodes                        */
+    int64_t table_used;     /* distinct nodes stored                          */
+    int64_t steps;          /* batched expansion steps                        */
+    int64_t exchanged;      /* nodes sent to other shards                     */
+    double seconds;         /* first expansion -> goal accepted (wall)        */
+    double expand_ms;       /* sum of expand-kernel durations (profile = 1)   */
+    int64_t expand_launches;
+    int64_t expand_parents; /* parents handed to the expand kernel            */
+} pastar_result;
+
+typedef struct pastar_ctx pastar_ctx;
+
+const char *pastar_last_error(void);
+int pastar_abi_version(void);
+
+/* ---- host-side helpers (reference file formats and precompute) ---- */
+
+/* read_fasta_file (read_fasta.cpp:8-56): a line that is empty or starts with
+ * '>' ends the current sequence; '\r' is kept.  Writes up to *n (in: capacity)
+ * sequences back to back into buf (cap bytes, no separators) and their
+ * lengths into lengths[]. */
+int pastar_read_fasta(const char *path, char *buf, int64_t cap, int *n, int *lengths);
+
+/* weightAltschulsRationale2 (WeightedSP.cpp:424-519): float n*n matrix. */
+int pastar_compute_weights(int n, const char *const *residues, const int *lengths, float *out);
+
+/* Cost::cost (Cost.cpp:266-270) of the reference table. */
+int pastar_cost(int r, int l);
+
+/* Coord<N>::get_id (CoordHash.cpp:191-245); -1 on an invalid shift. */
+int pastar_owner(int n, const uint16_t *pos, int size, int hash_type, int shift);
+
+/* ---- RCCL bootstrap (replaces MPI_Init + rank bookkeeping) ---- */
+int pastar_rccl_unique_id(unsigned char out[128]);
+
+/* ---- device context ---- */
+
+/* device: HIP ordinal; n_shards >= 1; shard_rank in [0, n_shards);
+ * rccl_id: 128 bytes from pastar_rccl_unique_id on rank 0 (NULL when
+ * n_shards == 1). */
+int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int shard_rank,
+                      const void *rccl_id, pastar_ctx **out);
+void pastar_gpu_destroy(pastar_ctx *ctx);
+
+/* Phase 1: PairAlign tables by the anti-diagonal wavefront kernel. */
+int pastar_gpu_build_heuristic(pastar_ctx *ctx);
+int pastar_gpu_pair_table(pastar_ctx *ctx, int pair, int32_t *out);
+int pastar_gpu_weights(pastar_ctx *ctx, int32_t *out);
+int pastar_gpu_h(pastar_ctx *ctx, const uint16_t *pos, int count, int32_t *out);
+
+/* Batched Node::getNeigh.  For each input node, every border-valid neighbour
+ * in increasing mask order, compacted back to back (input order preserved).
+ * out/out_owner/out_src need n_in * (2^n - 1) entries; out_owner receives
+ * get_id(vec_size), out_src the input index. */
+int pastar_gpu_expand(pastar_ctx *ctx, const pastar_node *in, int n_in, int vec_size,
+                      pastar_node *out, int32_t *out_owner, int32_t *out_src, int64_t *n_out);
+
+/* Device-resident PAStar search from the origin to the final coordinate. */
+int pastar_gpu_search(pastar_ctx *ctx, const pastar_search_opts *opts, pastar_result *res);
+
+/* ClosedList lookup after a search: the stored node for a coordinate owned by
+ * this shard (PASTAR_ENOTFOUND if absent). */
+int pastar_gpu_closed_lookup(pastar_ctx *ctx, const uint16_t *pos, pastar_node *out);
+
+/* Backtrace (backtrace.cpp:47-69 / PAStarDistributedBacktrace.cpp:19-213):
+ * the alignment rows, n rows of `stride` bytes each, NUL terminated; *cols
+ * receives the alignment length.  Collective over all shards. */
+int pastar_gpu_alignment(pastar_ctx *ctx, char *rows, int stride, int *cols);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,13 @@
+"""MI355X-native PAStar frontier-expansion engine.
+
+The search hot path of Gabrielcarvfer/mpi_pastar_msa (batched getNeigh, SP g,
+HPair h, dedup/relax into the Open/Closed table, owner routing between GPU
+shards) runs as hand-written HIP kernels for gfx950 behind the C-ABI in
+include/pastar_gpu.h.  This package is the Python host mirror of the
+reference interface; see pastar.py.
+"""
+from .pastar import (Engine, Node, PAStarOpt, SearchResult, Sequences, compute_weights, cost, get_id,
+                     rccl_unique_id, similarity)
+
+__all__ = ["Engine", "Node", "PAStarOpt", "SearchResult", "Sequences", "compute_weights", "cost", "get_id",
+           "rccl_unique_id", "similarity"]

@@ -1,0 +1,75 @@
+"""Build the native parts of the engine in-tree (hipcc for gfx950).
+
+  libpastar_gpu.so   HIP kernels + C-ABI (include/pastar_gpu.h)
+  bin/msa_pastar     C++ CLI mirroring the reference's msa_pastar
+
+The .so files land next to this file so that they travel with the repository
+snapshot to the GPU box (they are git-ignored, not gpurun-ignored).
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libpastar_gpu.so")
+CLI = os.path.join(HERE, "bin", "msa_pastar")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# -ffp-contract=off keeps the host weight pipeline in plain IEEE single
+# arithmetic (no FMA contraction), as the reference's g++ build computes it.
+COMMON = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+          "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+
+LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp"]
+LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build_lib(force=False):
+    deps = [os.path.join(CSRC, s) for s in LIB_DEPS] + [os.path.join(ROOT, "include", "pastar_gpu.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for s in LIB_SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(CSRC, os.path.splitext(s)[0] + ".o")
+        _run([HIPCC] + COMMON + ["-c", src, "-o", obj])
+        objs.append(obj)
+    _run([HIPCC, "--offload-arch=gfx950", "-shared", "-o", LIB] + objs +
+         ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+def build_cli(force=False):
+    src = os.path.join(CSRC, "msa_pastar_main.cpp")
+    deps = [src, LIB, os.path.join(ROOT, "include", "pastar_gpu.h")]
+    if not force and not _stale(CLI, deps):
+        return CLI
+    os.makedirs(os.path.dirname(CLI), exist_ok=True)
+    _run(["g++", "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), src, "-o", CLI,
+          "-L" + HERE, "-lpastar_gpu", "-Wl,-rpath,$ORIGIN/.."])
+    return CLI
+
+
+def build_all(force=False):
+    build_lib(force)
+    build_cli(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,397 @@
+// device.hpp -- gfx950 device code of the PAStar frontier-expansion engine.
+//
+// Layout in HBM (see DESIGN.md "Data layout"):
+//   DevProblem   problem constants (pair list, weights, key packing), read by
+//                uniform (scalar) loads
+//   H            PairAlign suffix tables, one row-major (L_x+1)*(L_y+1) int32
+//                block per pair
+//   codes / sub  residues as small integer codes + code x code distance table
+//   table        open-addressing node table (Open U Closed), one 32-B slot
+//                (64 B for 4-word keys):
+//                  word 0..KW-1  packed coordinate (bit 63 set = written)
+//                  word KW       best = g << 32 | parent mask  (atomicMin)
+//                  word KW+1     lo: closed_g (atomicMin), hi: h
+//   near / far   open piles of 8-B entries {slot, f}
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pastar {
+namespace dev {
+
+constexpr int kMaxN = 16;
+constexpr int kMaxPairs = kMaxN * (kMaxN - 1) / 2;
+constexpr int kHistBins = 1024;       // f histogram of the near pile
+constexpr int kBlock = 256;           // threads per block (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kTPerWave = 512;        // int2 pair-corner terms per wave (LDS)
+constexpr uint64_t kMark = 1ull << 63;  // key word written / occupied
+constexpr int kMaxProbe = 1 << 16;
+constexpr int kIntMax = 0x7fffffff;
+
+struct DevProblem {
+    int n, npairs, kw, alpha;
+    int gap_open, gap_ext, gap_gap;
+    int hash_type, hash_shift, n_shards, shard, pad0;
+    int len[kMaxN];
+    int kword[kMaxN], kshift[kMaxN], kbits[kMaxN];
+    uint64_t goal_key[4];
+    uint64_t origin_key[4];
+    int pair_x[kMaxPairs], pair_y[kMaxPairs], weight[kMaxPairs];
+    int h_row[kMaxPairs];
+    int64_t h_off[kMaxPairs];
+    int64_t seq_off[kMaxN];
+    const int32_t *H;
+    const uint8_t *codes;
+    const int32_t *sub;  // alpha x alpha
+};
+
+struct Entry {  // open-pile entry
+    uint32_t slot;
+    int32_t f;
+};
+
+// Per-step counters (two sets, alternating with the step parity).
+struct StepStats {
+    unsigned long long near_count;    // entries in the next near pile
+    unsigned long long far_count;     // entries appended to the far pile
+    unsigned long long batch_count;   // entries selected for expansion
+    unsigned long long expanded;      // parents that passed stale/closed checks
+    unsigned long long reopen;
+    unsigned long long generated;     // border-valid children
+    unsigned long long claimed;       // new table slots
+    unsigned long long outbox_total;
+    unsigned long long overflow;      // capacity or probe-limit failures
+    unsigned long long dropped;       // pruned by f >= bound / stale
+    unsigned long long pad[6];
+    unsigned long long outbox_count[8];
+    unsigned int hist[kHistBins];
+};
+
+struct FarStats {
+    int min_f;
+    int pad;
+    unsigned long long live;
+    unsigned int hist[kHistBins];
+};
+
+// Remote record sent to the owner shard over RCCL.
+template <int KW>
+struct Remote {
+    uint64_t key[KW];
+    int32_t g, h, pmask, pad;
+};
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+template <int KW>
+__device__ __forceinline__ uint64_t key_hash(const uint64_t (&k)[KW])
+{
+    uint64_t h = mix64(k[0]);
+#pragma unroll
+    for (int w = 1; w < KW; w++)
+        h = mix64(h ^ k[w]);
+    return h;
+}
+
+template <int KW>
+__host__ __device__ constexpr int slot_words()
+{
+    return KW <= 2 ? 4 : 8;
+}
+
+// Wave-aggregated append: one atomic per wave, lanes write compacted
+// (ballot + prefix popcount).  Must be reached by every lane of the wave.
+template <typename T>
+__device__ __forceinline__ void wave_append(bool pred, unsigned long long *counter, T *out,
+                                            unsigned long long cap, const T &v,
+                                            unsigned long long *overflow)
+{
+    const uint64_t mask = __ballot(pred);
+    if (!mask)
+        return;
+    const int lane = lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long base = 0;
+    if (lane == leader)
+        base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    if (pred) {
+        const unsigned long long idx = base + __popcll(mask & ((1ull << lane) - 1ull));
+        if (idx < cap)
+            out[idx] = v;
+        else if (overflow)
+            atomicAdd(overflow, 1ull);
+    }
+}
+
+// Relax (key, g, parent mask) into the node table.  Returns the slot (or -1
+// when the probe limit is hit) and sets `improved` when g is strictly better
+// than every g recorded for the key so far; `claimed` when the slot is new.
+//
+// Concurrency: slots are never freed, and every key word goes 0 -> final
+// exactly once, so a non-zero key word is always current and a plain load
+// may only lag (reading 0).  The claim is a CAS on word 0; 2- and 4-word keys
+// publish their tail words with agent-scope atomic stores, and a reader that
+// matched word 0 re-reads a zero tail word until it is written (the claimant
+// writes it in the same loop iteration, so no wave can stall on itself).
+// best only decreases, so a lagging read of it can only skip a relaxation
+// that would not improve anything.
+template <int KW>
+__device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t cap_mask,
+                                         const uint64_t (&key)[KW], int g, int pmask, int h,
+                                         bool &improved, bool &claimed)
+{
+    constexpr int SW = slot_words<KW>();
+    improved = false;
+    claimed = false;
+    uint64_t idx = key_hash<KW>(key) & cap_mask;
+    for (int probe = 0; probe < kMaxProbe;) {
+        uint64_t *s = table + idx * SW;
+        uint64_t w0 = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool mine = false;
+        if (w0 == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long *)s, 0ull, (unsigned long long)key[0]);
+            if (prev == 0) {
+#pragma unroll
+                for (int w = 1; w < KW; w++)
+                    __hip_atomic_store(s + w, key[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                reinterpret_cast<int32_t *>(s + KW + 1)[1] = h;
+                claimed = true;
+                mine = true;
+            } else {
+                w0 = prev;
+            }
+        }
+        if (!mine) {
+            if (w0 != key[0]) {
+                idx = (idx + 1) & cap_mask;
+                probe++;
+                continue;
+            }
+            bool same = true, pending = false;
+#pragma unroll
+            for (int w = 1; w < KW; w++) {
+                const uint64_t v = __hip_atomic_load(s + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pending |= (v == 0);
+                same &= (v == key[w]);
+            }
+            if (pending)
+                continue;  // tail still being published: re-read this slot
+            if (!same) {
+                idx = (idx + 1) & cap_mask;
+                probe++;
+                continue;
+            }
+        }
+        const uint64_t packed = ((uint64_t)(uint32_t)g << 32) | (uint32_t)pmask;
+        const uint64_t seen = s[KW];
+        if (packed < seen) {
+            const uint64_t old = atomicMin((unsigned long long *)(s + KW), (unsigned long long)packed);
+            improved = (int64_t)(old >> 32) > (int64_t)g || old == ~0ull;
+        }
+        return (int64_t)idx;
+    }
+    return -1;
+}
+
+// Lookup without insertion (closed list / backtrace).
+template <int KW>
+__device__ __forceinline__ int64_t lookup(const uint64_t *__restrict__ table, uint64_t cap_mask,
+                                          const uint64_t (&key)[KW])
+{
+    constexpr int SW = slot_words<KW>();
+    uint64_t idx = key_hash<KW>(key) & cap_mask;
+    for (int probe = 0; probe < kMaxProbe; probe++) {
+        const uint64_t *s = table + idx * SW;
+        if (s[0] == 0)
+            return -1;
+        bool same = true;
+#pragma unroll
+        for (int w = 0; w < KW; w++)
+            same &= (s[w] == key[w]);
+        if (same)
+            return (int64_t)idx;
+        idx = (idx + 1) & cap_mask;
+    }
+    return -1;
+}
+
+// ---------------------------------------------------------------------------
+// CoordHash owner (CoordHash.cpp:107-245) on device, for the shard partition.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int ilog2_floor(int v) { return 31 - __clz(v); }
+
+template <int NMAX>
+__device__ __forceinline__ int owner_dev(const DevProblem &P, int n, const int (&pos)[NMAX], int size)
+{
+    if (size <= 1)
+        return 0;
+    const int shift = P.hash_shift;
+    if (P.hash_type == 2 || P.hash_type == 3) {
+        unsigned s = 0;
+        const int lim = P.hash_type == 2 ? n : 2;
+#pragma unroll
+        for (int i = 0; i < NMAX; i++)
+            if (i < lim)
+                s += (unsigned)pos[i];
+        return (int)((s >> shift) % (unsigned)size);
+    }
+    const int dims = P.hash_type == 1 ? 2 : n;
+    // (unsigned)(log2(size) + shift % dims + 1): exact for integer log2 of a
+    // power of two, floor otherwise (log2 of a non-power is not an integer).
+    const unsigned bits = (unsigned)(ilog2_floor(size) + (shift % dims) + 1);
+    const unsigned total = bits >= 31 ? 0x80000000u : (1u << bits);
+    int hash = 0;
+    int bit_to_read = shift / dims;
+    for (unsigned bit = 1; bit != 0 && bit <= total;) {
+        for (int j = 0; j < dims && bit != 0 && bit <= total; ++j) {
+            int c = 0;
+#pragma unroll
+            for (int i = 0; i < NMAX; i++)
+                if (i == j)
+                    c = pos[i];
+            if (bit_to_read < 16 && (c & (1 << bit_to_read)))
+                hash = (int)((unsigned)hash | bit);
+            bit <<= 1;
+        }
+        ++bit_to_read;
+    }
+    return (int)((unsigned)((hash >> (shift % dims)) % size));
+}
+
+// ---------------------------------------------------------------------------
+// Parent setup: decode the coordinate and stage the 4 corner terms of every
+// pair in LDS.  For a parent p and neighbour mask m, pair (x, y) contributes
+//   g: w * {GapGap, gap(x idle), gap(y idle), cost(s_x[p_x], s_y[p_y])}
+//   h: w * H_xy[p_x + b_x][p_y + b_y]
+// selected by corner c = b_x << 1 | b_y (Node.cpp:130-152, 206-248;
+// HeuristicHPair.cpp:74-86).  One expansion reads 4P H cells, not 4P per
+// neighbour.
+// ---------------------------------------------------------------------------
+template <int N, int KW>
+struct Parent {
+    static constexpr int NMAX = N ? N : kMaxN;
+    uint64_t key[KW];
+    int pos[NMAX];
+    int g, pmask, blocked;
+};
+
+template <int N, int KW>
+__device__ __forceinline__ void decode_key(const DevProblem &P, int n, const uint64_t (&key)[KW],
+                                           int (&pos)[Parent<N, KW>::NMAX])
+{
+#pragma unroll
+    for (int i = 0; i < Parent<N, KW>::NMAX; i++) {
+        if (N == 0 && i >= n) {
+            pos[i] = 0;
+            continue;
+        }
+        const int w = P.kword[i];
+        uint64_t word = key[0];
+#pragma unroll
+        for (int k = 1; k < KW; k++)
+            if (w == k)
+                word = key[k];
+        pos[i] = (int)((word >> P.kshift[i]) & ((1ull << P.kbits[i]) - 1ull));
+    }
+}
+
+// Fills terms[q], q = p*4 + c, for q in [glane, 4P) step lpn.
+template <int N, int KW>
+__device__ __forceinline__ void stage_terms(const DevProblem &P, int n, int npairs,
+                                            const Parent<N, KW> &par, int2 *terms, int glane, int lpn)
+{
+    for (int q = glane; q < 4 * npairs; q += lpn) {
+        const int p = q >> 2, c = q & 3;
+        const int x = P.pair_x[p], y = P.pair_y[p], w = P.weight[p];
+        int px = 0, py = 0;
+#pragma unroll
+        for (int i = 0; i < Parent<N, KW>::NMAX; i++) {
+            if (i == x)
+                px = par.pos[i];
+            if (i == y)
+                py = par.pos[i];
+        }
+        const int bx = c >> 1, by = c & 1;
+        int gc, hc = 0;
+        if (c == 3) {
+            const int lx = P.len[x], ly = P.len[y];
+            const int ax = P.codes[P.seq_off[x] + (px < lx ? px : lx)];
+            const int ay = P.codes[P.seq_off[y] + (py < ly ? py : ly)];
+            gc = P.sub[ax * P.alpha + ay];
+        } else if (c == 2) {  // x moves, y idle: open iff y moved into the parent
+            gc = ((par.pmask >> y) & 1) ? P.gap_open : P.gap_ext;
+        } else if (c == 1) {
+            gc = ((par.pmask >> x) & 1) ? P.gap_open : P.gap_ext;
+        } else {
+            gc = P.gap_gap;
+        }
+        if (px + bx <= P.len[x] && py + by <= P.len[y])
+            hc = P.H[P.h_off[p] + (int64_t)(px + bx) * P.h_row[p] + (py + by)];
+        terms[q] = make_int2(gc * w, hc * w);
+    }
+}
+
+// Sum of the staged terms for neighbour mask m: (delta g, h).
+template <int N>
+__device__ __forceinline__ int2 child_cost(const DevProblem &P, int npairs, const int2 *terms, int m)
+{
+    int dg = 0, hh = 0;
+    if constexpr (N > 0) {
+        int p = 0;
+#pragma unroll
+        for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+            for (int y = x + 1; y < N; y++, p++) {
+                const int c = (((m >> x) & 1) << 1) | ((m >> y) & 1);
+                const int2 t = terms[p * 4 + c];
+                dg += t.x;
+                hh += t.y;
+            }
+        }
+    } else {
+        for (int p = 0; p < npairs; p++) {
+            const int x = P.pair_x[p], y = P.pair_y[p];
+            const int c = (((m >> x) & 1) << 1) | ((m >> y) & 1);
+            const int2 t = terms[p * 4 + c];
+            dg += t.x;
+            hh += t.y;
+        }
+    }
+    return make_int2(dg, hh);
+}
+
+template <int N, int KW>
+__device__ __forceinline__ void child_key(const DevProblem &P, int n, const uint64_t (&key)[KW], int m,
+                                          uint64_t (&out)[KW])
+{
+#pragma unroll
+    for (int w = 0; w < KW; w++)
+        out[w] = key[w];
+#pragma unroll
+    for (int i = 0; i < Parent<N, KW>::NMAX; i++) {
+        if ((N == 0 && i >= n) || !((m >> i) & 1))
+            continue;
+        const uint64_t inc = 1ull << P.kshift[i];
+        const int w = P.kword[i];
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            if (w == k)
+                out[k] += inc;
+    }
+}
+
+}  // namespace dev
+}  // namespace pastar

@@ -1,0 +1,1126 @@
+// pastar_gpu.hip -- host side of the C-ABI (include/pastar_gpu.h): device
+// context, Phase 1 (PairAlign wavefront), the batched expansion API and the
+// device-resident search loop with the RCCL shard exchange.
+//
+// Search loop, one step (DESIGN.md "Search step"):
+//   partition_kernel   near pile -> batch (f <= t) + next near pile
+//   expand_kernel      batch -> neighbours relaxed into the node table;
+//                      improved ones appended to near (f < t_near) / far;
+//                      remote-owned ones posted to per-shard outboxes
+//   [n_shards > 1]     RCCL send/recv of the outboxes, insert_remote_kernel,
+//                      allreduce of {goal g, remaining work}
+//   status D2H         counters + near histogram -> next t, refill decision
+// Termination: no open entry with f < best goal g remains on any shard
+// (PAStar::check_stop's goal-f <= every open f, PAStar.cpp:480-547).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host_model.hpp"
+#include "kernels.hpp"
+#include "pastar_gpu.h"
+
+using namespace pastar;
+using namespace pastar::dev;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail(PASTAR_ENODEV, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+                        __FILE__, __LINE__);                                                       \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                             \
+    do {                                                                                           \
+        ncclResult_t _r = (expr);                                                                  \
+        if (_r != ncclSuccess)                                                                     \
+            return fail(PASTAR_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(_r));            \
+    } while (0)
+
+#define PA_TRY(expr)          \
+    do {                      \
+        int _rc = (expr);     \
+        if (_rc != PASTAR_OK) \
+            return _rc;       \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { reset(); }
+    void reset()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    int alloc(size_t count)
+    {
+        reset();
+        if (count == 0)
+            return PASTAR_OK;
+        hipError_t e = hipMalloc(&p, sizeof(T) * count);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(PASTAR_ENOMEM, "hipMalloc(%zu bytes) failed: %s", sizeof(T) * count, hipGetErrorString(e));
+        }
+        n = count;
+        return PASTAR_OK;
+    }
+};
+
+double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct pastar_ctx {
+    int device = 0, n_shards = 1, shard = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    // problem
+    int n = 0, npairs = 0, kw = 1;
+    std::vector<std::string> seqs;
+    std::vector<int> weights;
+    DevProblem hp{};
+    DevBuf<DevProblem> dP;
+    DevBuf<int32_t> dH;
+    DevBuf<uint8_t> dcodes;
+    DevBuf<int32_t> dsub;
+    bool heuristic_ready = false;
+
+    // search state
+    DevBuf<uint64_t> table;
+    uint64_t nslots = 0;
+    DevBuf<Entry> near_buf[2], far_buf[2], batch;
+    DevBuf<StepStats> stats;  // [0], [1] step parity, [2] refill
+    DevBuf<FarStats> farstats;
+    DevBuf<unsigned long long> far_n;
+    DevBuf<int> goal;
+    DevBuf<uint8_t> outbox, inbox;
+    DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
+    StepStats *h_stats = nullptr;         // pinned
+    FarStats *h_far = nullptr;            // pinned
+    bool searched = false;
+    int64_t score = -1;
+};
+
+namespace {
+
+int slot_words_rt(int kw) { return kw <= 2 ? 4 : 8; }
+
+// ---------------------------------------------------------------------------
+// Problem setup (host)
+// ---------------------------------------------------------------------------
+int setup_problem(pastar_ctx *c, const pastar_problem *p)
+{
+    if (!p || p->n < 2 || p->n > PASTAR_MAX_SEQ || !p->lengths || !p->residues)
+        return fail(PASTAR_EINVAL, "invalid problem (n=%d)", p ? p->n : -1);
+    c->n = p->n;
+    c->npairs = p->n * (p->n - 1) / 2;
+    for (int i = 0; i < p->n; i++) {
+        if (p->lengths[i] < 1 || p->lengths[i] > 8000 || !p->residues[i])
+            return fail(PASTAR_EINVAL, "sequence %d: length %d outside [1, 8000]", i, p->lengths[i]);
+        c->seqs.emplace_back(p->residues[i], (size_t)p->lengths[i]);
+    }
+    if (p->hash_shift < 0 || p->hash_shift > 21)
+        return fail(PASTAR_EINVAL, "Invalid Hash Shift %d", p->hash_shift);
+    if (p->hash_type < 0 || p->hash_type > 3)
+        return fail(PASTAR_EINVAL, "Invalid hash type %d", p->hash_type);
+
+    // pair weights: given, or Altschul rationale-2 on the host
+    if (p->weights) {
+        c->weights.assign(p->weights, p->weights + c->npairs);
+    } else {
+        std::vector<float> wf = altschul_weights(c->seqs);
+        for (int x = 0; x < c->n - 1; x++)
+            for (int y = x + 1; y < c->n; y++)
+                c->weights.push_back((int)wf[(size_t)x * c->n + y]);
+    }
+
+    DevProblem &hp = c->hp;
+    std::memset(&hp, 0, sizeof(hp));
+    hp.n = c->n;
+    hp.npairs = c->npairs;
+    hp.gap_open = p->gap_open;
+    hp.gap_ext = p->gap_ext;
+    hp.gap_gap = p->gap_gap;
+    hp.hash_type = p->hash_type;
+    hp.hash_shift = p->hash_shift;
+    hp.n_shards = c->n_shards;
+    hp.shard = c->shard;
+
+    // residue codes: every byte value present, plus code 0 for the string end
+    int code_of[256];
+    for (int i = 0; i < 256; i++)
+        code_of[i] = -1;
+    std::vector<int> chars = {0};
+    code_of[0] = 0;
+    for (const auto &s : c->seqs)
+        for (unsigned char ch : s)
+            if (code_of[ch] < 0) {
+                code_of[ch] = (int)chars.size();
+                chars.push_back(ch);
+            }
+    hp.alpha = (int)chars.size();
+    std::vector<int32_t> sub((size_t)hp.alpha * hp.alpha);
+    for (int a = 0; a < hp.alpha; a++)
+        for (int b = 0; b < hp.alpha; b++) {
+            const int r = chars[a], l = chars[b];
+            int v;
+            if (p->sub)
+                v = (r < 128 && l < 128) ? p->sub[r * 128 + l] : 0;
+            else
+                v = ref_cost((signed char)r, (signed char)l);
+            sub[(size_t)a * hp.alpha + b] = v;
+        }
+    std::vector<uint8_t> codes;
+    int64_t off = 0;
+    for (int i = 0; i < c->n; i++) {
+        hp.len[i] = (int)c->seqs[i].size();
+        hp.seq_off[i] = off;
+        for (unsigned char ch : c->seqs[i])
+            codes.push_back((uint8_t)code_of[ch]);
+        codes.push_back(0);
+        off += (int64_t)c->seqs[i].size() + 1;
+    }
+
+    // key packing: coordinates never straddle a word; bit 63 marks a word
+    int word = 0, used = 0;
+    for (int i = 0; i < c->n; i++) {
+        int bits = 1;
+        while ((1 << bits) <= hp.len[i])
+            bits++;
+        if (used + bits > 63) {
+            word++;
+            used = 0;
+        }
+        hp.kword[i] = word;
+        hp.kshift[i] = used;
+        hp.kbits[i] = bits;
+        used += bits;
+    }
+    const int words = word + 1;
+    c->kw = words <= 1 ? 1 : (words <= 2 ? 2 : (words <= 4 ? 4 : -1));
+    if (c->kw < 0)
+        return fail(PASTAR_EINVAL, "coordinate key needs %d words (> 4)", words);
+    hp.kw = c->kw;
+    for (int w = 0; w < 4; w++)
+        hp.goal_key[w] = hp.origin_key[w] = (w < c->kw) ? kMark : 0;
+    for (int i = 0; i < c->n; i++)
+        hp.goal_key[hp.kword[i]] += (uint64_t)hp.len[i] << hp.kshift[i];
+
+    int64_t hoff = 0, k = 0;
+    for (int x = 0; x < c->n - 1; x++)
+        for (int y = x + 1; y < c->n; y++, k++) {
+            hp.pair_x[k] = x;
+            hp.pair_y[k] = y;
+            hp.weight[k] = c->weights[k];
+            hp.h_row[k] = hp.len[y] + 1;
+            hp.h_off[k] = hoff;
+            hoff += (int64_t)(hp.len[x] + 1) * (hp.len[y] + 1);
+        }
+
+    PA_TRY(c->dH.alloc((size_t)hoff));
+    PA_TRY(c->dcodes.alloc(codes.size()));
+    PA_TRY(c->dsub.alloc(sub.size()));
+    PA_TRY(c->dP.alloc(1));
+    hp.H = c->dH.p;
+    hp.codes = c->dcodes.p;
+    hp.sub = c->dsub.p;
+    HIP_TRY(hipMemcpy(c->dcodes.p, codes.data(), codes.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->dsub.p, sub.data(), sub.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->dP.p, &hp, sizeof(hp), hipMemcpyHostToDevice));
+    return PASTAR_OK;
+}
+
+void pack_key(const pastar_ctx *c, const uint16_t *pos, uint64_t *key)
+{
+    for (int w = 0; w < 4; w++)
+        key[w] = (w < c->kw) ? kMark : 0;
+    for (int i = 0; i < c->n; i++)
+        key[c->hp.kword[i]] += (uint64_t)pos[i] << c->hp.kshift[i];
+}
+
+int check_launch()
+{
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(PASTAR_ENODEV, "kernel launch failed: %s", hipGetErrorString(e));
+    return PASTAR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Per-(N, KW) dispatch
+// ---------------------------------------------------------------------------
+struct Ops {
+    void (*expand_api)(dim3, dim3, hipStream_t, const DevProblem *, const pastar_node *, int, const int64_t *, int,
+                       pastar_node *, int32_t *, int32_t *);
+    void (*expand)(dim3, dim3, hipStream_t, const SearchArgs &);
+    void (*insert_remote)(dim3, dim3, hipStream_t, const SearchArgs &, const void *, unsigned long long);
+    void (*walk)(hipStream_t, const DevProblem *, const uint64_t *, uint64_t, const uint64_t *, int, int, int32_t *,
+                 uint64_t *, int *);
+    void (*lookup)(hipStream_t, const uint64_t *, uint64_t, const uint64_t *, uint64_t *);
+};
+
+template <int N, int KW>
+struct Impl {
+    static void expand_api(dim3 g, dim3 b, hipStream_t s, const DevProblem *P, const pastar_node *in, int n_in,
+                           const int64_t *off, int vec, pastar_node *out, int32_t *own, int32_t *src)
+    {
+        hipLaunchKernelGGL((expand_api_kernel<N, KW>), g, b, 0, s, P, in, n_in, off, vec, out, own, src);
+    }
+    static void expand(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a)
+    {
+        hipLaunchKernelGGL((expand_kernel<N, KW>), g, b, 0, s, a);
+    }
+    static void insert_remote(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a, const void *recs,
+                              unsigned long long count)
+    {
+        hipLaunchKernelGGL((insert_remote_kernel<KW>), g, b, 0, s, a, (const Remote<KW> *)recs, count);
+    }
+    static void walk(hipStream_t s, const DevProblem *P, const uint64_t *t, uint64_t cm, const uint64_t *start, int max,
+                     int local, int32_t *masks, uint64_t *last, int *info)
+    {
+        hipLaunchKernelGGL((walk_kernel<N, KW>), dim3(1), dim3(1), 0, s, P, t, cm, start, max, local, masks, last, info);
+    }
+    static void lookup(hipStream_t s, const uint64_t *t, uint64_t cm, const uint64_t *key, uint64_t *out)
+    {
+        hipLaunchKernelGGL((lookup_kernel<KW>), dim3(1), dim3(1), 0, s, t, cm, key, out);
+    }
+    static Ops ops() { return Ops{expand_api, expand, insert_remote, walk, lookup}; }
+};
+
+template <int KW>
+Ops ops_for_kw(int n)
+{
+    switch (n) {
+    case 3: return Impl<3, KW>::ops();
+    case 4: return Impl<4, KW>::ops();
+    case 5: return Impl<5, KW>::ops();
+    case 6: return Impl<6, KW>::ops();
+    case 7: return Impl<7, KW>::ops();
+    case 8: return Impl<8, KW>::ops();
+    default: return Impl<0, KW>::ops();
+    }
+}
+
+Ops ops_for(const pastar_ctx *c)
+{
+    if (c->kw == 1)
+        return ops_for_kw<1>(c->n);
+    if (c->kw == 2)
+        return ops_for_kw<2>(c->n);
+    return ops_for_kw<4>(c->n);
+}
+
+size_t remote_bytes(int kw) { return (size_t)kw * 8 + 16; }
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+const char *pastar_last_error(void) { return g_err.c_str(); }
+int pastar_abi_version(void) { return PASTAR_ABI_VERSION; }
+
+int pastar_cost(int r, int l) { return ref_cost(r, l); }
+
+int pastar_owner(int n, const uint16_t *pos, int size, int hash_type, int shift)
+{
+    if (!pos || n < 2 || n > PASTAR_MAX_SEQ)
+        return -1;
+    return owner_of(n, pos, size, hash_type, shift);
+}
+
+int pastar_read_fasta(const char *path, char *buf, int64_t cap, int *n, int *lengths)
+{
+    if (!path || !n)
+        return fail(PASTAR_EINVAL, "null argument");
+    std::vector<std::string> seqs;
+    if (!read_fasta(path, seqs))
+        return fail(PASTAR_EIO, "Can't open file %s", path);
+    if ((int)seqs.size() > *n)
+        return fail(PASTAR_EINVAL, "%zu sequences exceed capacity %d", seqs.size(), *n);
+    int64_t off = 0;
+    for (size_t i = 0; i < seqs.size(); i++) {
+        if (off + (int64_t)seqs[i].size() > cap)
+            return fail(PASTAR_EINVAL, "residue buffer too small");
+        if (buf)
+            std::memcpy(buf + off, seqs[i].data(), seqs[i].size());
+        if (lengths)
+            lengths[i] = (int)seqs[i].size();
+        off += (int64_t)seqs[i].size();
+    }
+    *n = (int)seqs.size();
+    return PASTAR_OK;
+}
+
+int pastar_compute_weights(int n, const char *const *residues, const int *lengths, float *out)
+{
+    if (n < 2 || n > PASTAR_MAX_SEQ || !residues || !lengths || !out)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    std::vector<std::string> seqs;
+    for (int i = 0; i < n; i++)
+        seqs.emplace_back(residues[i], (size_t)lengths[i]);
+    std::vector<float> w = altschul_weights(seqs);
+    std::memcpy(out, w.data(), sizeof(float) * (size_t)n * n);
+    return PASTAR_OK;
+}
+
+int pastar_rccl_unique_id(unsigned char out[128])
+{
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(out, &id, sizeof(id));
+    return PASTAR_OK;
+}
+
+int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int shard_rank, const void *rccl_id,
+                      pastar_ctx **out)
+{
+    if (!out)
+        return fail(PASTAR_EINVAL, "null out");
+    *out = nullptr;
+    if (n_shards < 1 || n_shards > 8 || shard_rank < 0 || shard_rank >= n_shards)
+        return fail(PASTAR_EINVAL, "invalid shard %d of %d (1..8 shards)", shard_rank, n_shards);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(PASTAR_ENODEV, "no HIP device available (the engine has no CPU fallback)");
+    if (device < 0 || device >= ndev)
+        return fail(PASTAR_ENODEV, "device %d out of range (%d devices)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(PASTAR_ENODEV, "device %d is %s; this build targets gfx950 only", device, prop.gcnArchName);
+    std::unique_ptr<pastar_ctx> c(new pastar_ctx());
+    c->device = device;
+    c->n_shards = n_shards;
+    c->shard = shard_rank;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&c->ev0));
+    HIP_TRY(hipEventCreate(&c->ev1));
+    PA_TRY(setup_problem(c.get(), p));
+    if (n_shards > 1) {
+        if (!rccl_id)
+            return fail(PASTAR_EINVAL, "rccl_id required for n_shards > 1");
+        ncclUniqueId id;
+        std::memcpy(&id, rccl_id, sizeof(id));
+        NCCL_TRY(ncclCommInitRank(&c->comm, n_shards, id, shard_rank));
+    }
+    HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->h_far, sizeof(FarStats), hipHostMallocDefault));
+    *out = c.release();
+    return PASTAR_OK;
+}
+
+void pastar_gpu_destroy(pastar_ctx *c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    if (c->stream)
+        (void)hipStreamSynchronize(c->stream);
+    if (c->comm)
+        ncclCommDestroy(c->comm);
+    if (c->h_stats)
+        (void)hipHostFree(c->h_stats);
+    if (c->h_far)
+        (void)hipHostFree(c->h_far);
+    if (c->ev0)
+        (void)hipEventDestroy(c->ev0);
+    if (c->ev1)
+        (void)hipEventDestroy(c->ev1);
+    if (c->stream)
+        (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int pastar_gpu_build_heuristic(pastar_ctx *c)
+{
+    if (!c)
+        return fail(PASTAR_EINVAL, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    int maxl1 = 0;
+    for (int k = 0; k < c->npairs; k++)
+        maxl1 = std::max(maxl1, c->hp.len[c->hp.pair_x[k]]);
+    const size_t lds = (size_t)3 * (maxl1 + 1) * (sizeof(int) + 1) + 16;
+    if (lds > 160 * 1024)
+        return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl1);
+    if (lds > 64 * 1024)
+        HIP_TRY(hipFuncSetAttribute((const void *)pairalign_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(pairalign_kernel, dim3(c->npairs), dim3(kBlock), lds, c->stream, c->dP.p, c->dH.p);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->heuristic_ready = true;
+    return PASTAR_OK;
+}
+
+int pastar_gpu_pair_table(pastar_ctx *c, int pair, int32_t *out)
+{
+    if (!c || !out || pair < 0 || pair >= c->npairs)
+        return fail(PASTAR_EINVAL, "invalid pair %d", pair);
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t cells = (size_t)(c->hp.len[c->hp.pair_x[pair]] + 1) * (c->hp.len[c->hp.pair_y[pair]] + 1);
+    HIP_TRY(hipMemcpy(out, c->dH.p + c->hp.h_off[pair], cells * 4, hipMemcpyDeviceToHost));
+    return PASTAR_OK;
+}
+
+int pastar_gpu_weights(pastar_ctx *c, int32_t *out)
+{
+    if (!c || !out)
+        return fail(PASTAR_EINVAL, "null argument");
+    std::memcpy(out, c->weights.data(), sizeof(int32_t) * c->weights.size());
+    return PASTAR_OK;
+}
+
+int pastar_gpu_h(pastar_ctx *c, const uint16_t *pos, int count, int32_t *out)
+{
+    if (!c || !pos || !out || count < 0)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    if (count == 0)
+        return PASTAR_OK;
+    for (int k = 0; k < count; k++)
+        for (int i = 0; i < c->n; i++)
+            if (pos[(size_t)k * PASTAR_MAX_SEQ + i] > c->hp.len[i])
+                return fail(PASTAR_EINVAL, "coordinate %d outside the lattice", k);
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf<uint16_t> dpos;
+    DevBuf<int32_t> dout;
+    PA_TRY(dpos.alloc((size_t)count * PASTAR_MAX_SEQ));
+    PA_TRY(dout.alloc((size_t)count));
+    HIP_TRY(hipMemcpy(dpos.p, pos, (size_t)count * PASTAR_MAX_SEQ * 2, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(h_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream, c->dP.p, dpos.p, count, dout.p);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(out, dout.p, (size_t)count * 4, hipMemcpyDeviceToHost));
+    return PASTAR_OK;
+}
+
+int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_size, pastar_node *out,
+                      int32_t *out_owner, int32_t *out_src, int64_t *n_out)
+{
+    if (!c || (!in && n_in) || n_in < 0 || !n_out || vec_size < 1)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    *n_out = 0;
+    if (n_in == 0)
+        return PASTAR_OK;
+    // per-node output offsets: 2^(free dimensions) - 1 neighbours each
+    std::vector<int64_t> off((size_t)n_in);
+    int64_t total = 0;
+    for (int k = 0; k < n_in; k++) {
+        int free_dims = 0;
+        for (int i = 0; i < c->n; i++) {
+            if (in[k].pos[i] > c->hp.len[i])
+                return fail(PASTAR_EINVAL, "node %d outside the lattice", k);
+            free_dims += in[k].pos[i] < c->hp.len[i];
+        }
+        off[k] = total;
+        total += (1ll << free_dims) - 1;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf<pastar_node> din, dout;
+    DevBuf<int64_t> doff;
+    DevBuf<int32_t> down, dsrc;
+    PA_TRY(din.alloc((size_t)n_in));
+    PA_TRY(doff.alloc((size_t)n_in));
+    PA_TRY(dout.alloc((size_t)std::max<int64_t>(total, 1)));
+    PA_TRY(down.alloc((size_t)std::max<int64_t>(total, 1)));
+    PA_TRY(dsrc.alloc((size_t)std::max<int64_t>(total, 1)));
+    HIP_TRY(hipMemcpy(din.p, in, sizeof(pastar_node) * (size_t)n_in, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(doff.p, off.data(), sizeof(int64_t) * (size_t)n_in, hipMemcpyHostToDevice));
+    const int lpn = std::min(64, 1 << c->n);
+    const int per_block = kWaves * (64 / lpn);
+    const int blocks = std::min(4096, (n_in + per_block - 1) / per_block);
+    ops_for(c).expand_api(dim3(blocks), dim3(kBlock), c->stream, c->dP.p, din.p, n_in, doff.p, vec_size, dout.p,
+                          down.p, dsrc.p);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (total) {
+        if (out)
+            HIP_TRY(hipMemcpy(out, dout.p, sizeof(pastar_node) * (size_t)total, hipMemcpyDeviceToHost));
+        if (out_owner)
+            HIP_TRY(hipMemcpy(out_owner, down.p, 4 * (size_t)total, hipMemcpyDeviceToHost));
+        if (out_src)
+            HIP_TRY(hipMemcpy(out_src, dsrc.p, 4 * (size_t)total, hipMemcpyDeviceToHost));
+    }
+    *n_out = total;
+    return PASTAR_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Search
+// ===========================================================================
+namespace {
+
+struct SearchCfg {
+    unsigned long long kmax, near_cap, far_cap, outbox_cap;
+    int table_log2;
+    int verbose, profile;
+    int64_t max_steps;
+};
+
+int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
+{
+    const int sw = slot_words_rt(c->kw);
+    c->nslots = 1ull << cfg.table_log2;
+    PA_TRY(c->table.alloc((size_t)c->nslots * sw));
+    PA_TRY(c->near_buf[0].alloc(cfg.near_cap));
+    PA_TRY(c->near_buf[1].alloc(cfg.near_cap));
+    PA_TRY(c->far_buf[0].alloc(cfg.far_cap));
+    PA_TRY(c->far_buf[1].alloc(cfg.far_cap));
+    PA_TRY(c->batch.alloc(cfg.kmax));
+    PA_TRY(c->stats.alloc(3));
+    PA_TRY(c->farstats.alloc(1));
+    PA_TRY(c->far_n.alloc(1));
+    PA_TRY(c->goal.alloc(1));
+    if (c->n_shards > 1) {
+        const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
+        PA_TRY(c->outbox.alloc(bytes));
+        PA_TRY(c->inbox.alloc(bytes));
+        PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
+    }
+    const int blocks = (int)std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock);
+    if (sw == 4)
+        hipLaunchKernelGGL((init_table_kernel<4>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
+    else
+        hipLaunchKernelGGL((init_table_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats) * 3, c->stream));
+    HIP_TRY(hipMemsetAsync(c->far_n.p, 0, sizeof(unsigned long long), c->stream));
+    const int inf = kIntMax;
+    HIP_TRY(hipMemcpyAsync(c->goal.p, &inf, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    return PASTAR_OK;
+}
+
+// choose the batch threshold: smallest f with at least `target` entries <= f
+int pick_threshold(const unsigned int *hist, int base, unsigned long long target, unsigned long long *selected,
+                   int *fmin)
+{
+    unsigned long long cum = 0;
+    int first = -1;
+    for (int b = 0; b < kHistBins; b++) {
+        if (hist[b] && first < 0)
+            first = b;
+        cum += hist[b];
+        if (cum >= target && first >= 0) {
+            *selected = cum;
+            *fmin = base + first;
+            return base + b;
+        }
+    }
+    *selected = cum;
+    *fmin = first < 0 ? kIntMax : base + first;
+    return base + kHistBins - 1;
+}
+
+int allreduce_i64(pastar_ctx *c, int64_t *vals, int count, ncclRedOp_t op)
+{
+    DevBuf<int64_t> d;
+    PA_TRY(d.alloc((size_t)count));
+    HIP_TRY(hipMemcpyAsync(d.p, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
+    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, op, c->comm, c->stream));
+    HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
+template <int KWv>
+int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
+{
+    constexpr int KW = KWv;
+    const Ops ops = ops_for(c);
+    const int G = c->n_shards;
+    PA_TRY(alloc_search(c, cfg));
+    const int lpn = std::min(64, 1 << c->n);
+    const int per_block = kWaves * (64 / lpn);
+    const size_t rb = remote_bytes(KW);
+
+    // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
+    // its owner shard
+    uint16_t zero[PASTAR_MAX_SEQ] = {0};
+    const int origin_owner = G > 1 ? owner_of(c->n, zero, G, c->hp.hash_type, c->hp.hash_shift) : 0;
+    int32_t h0 = 0;
+    {
+        DevBuf<uint16_t> dpos;
+        DevBuf<int32_t> dh;
+        PA_TRY(dpos.alloc(PASTAR_MAX_SEQ));
+        PA_TRY(dh.alloc(1));
+        HIP_TRY(hipMemcpyAsync(dpos.p, zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(h_kernel, dim3(1), dim3(64), 0, c->stream, c->dP.p, dpos.p, 1, dh.p);
+        PA_TRY(check_launch());
+        HIP_TRY(hipMemcpyAsync(&h0, dh.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    int cur = 0, fcur = 0;
+    unsigned long long nn = 0, nf = 0;
+    int base = h0;  // histogram base of near[cur]
+    std::vector<unsigned int> hist(kHistBins, 0);
+    int t_near = h0 + kHistBins - 1;
+    int goal_g = kIntMax;
+
+    SearchArgs a{};
+    a.P = c->dP.p;
+    a.table = c->table.p;
+    a.cap_mask = c->nslots - 1;
+    a.batch = c->batch.p;
+    a.kmax = cfg.kmax;
+    a.near_cap = cfg.near_cap;
+    a.far_n = c->far_n.p;
+    a.far_cap = cfg.far_cap;
+    a.outbox = c->outbox.p;
+    a.outbox_cap = cfg.outbox_cap;
+    a.goal_g = c->goal.p;
+
+    if (c->shard == origin_owner) {
+        // relax the origin through the same insert path as remote records
+        std::vector<uint8_t> rec(rb, 0);
+        uint64_t key[4];
+        pack_key(c, zero, key);
+        std::memcpy(rec.data(), key, 8 * KW);
+        int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
+        std::memcpy(rec.data() + 8 * KW, tail, 16);
+        DevBuf<uint8_t> drec;
+        PA_TRY(drec.alloc(rb));
+        HIP_TRY(hipMemcpyAsync(drec.p, rec.data(), rb, hipMemcpyHostToDevice, c->stream));
+        a.st = c->stats.p + 0;
+        a.near_out = c->near_buf[0].p;
+        a.far_out = c->far_buf[0].p;
+        a.t_near = t_near;
+        a.bound = kIntMax;
+        a.base = base;
+        ops.insert_remote(dim3(1), dim3(kBlock), c->stream, a, drec.p, 1);
+        PA_TRY(check_launch());
+        HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        nn = c->h_stats->near_count;
+        std::memcpy(hist.data(), c->h_stats->hist, sizeof(unsigned int) * kHistBins);
+        HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
+    }
+
+    int64_t expanded = 0, reopen = 0, generated = 0, claimed = 0, exchanged = 0, steps = 0;
+    double expand_ms = 0;
+    int64_t launches = 0, parents = 0;
+    const double t0 = now_s();
+    bool done = false;
+    while (!done) {
+        if (cfg.max_steps && steps >= cfg.max_steps)
+            return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
+        const int par = (int)(steps & 1);
+        StepStats *st = c->stats.p + par;
+        StepStats *st_next = c->stats.p + (1 - par);
+        unsigned long long sel = 0;
+        int fmin = kIntMax;
+        int t = base - 1;
+        if (nn > 0)
+            t = pick_threshold(hist.data(), base, cfg.kmax, &sel, &fmin);
+        const int bound = goal_g;
+        const int new_base = nn > 0 ? fmin : base;
+        a.st = st;
+        a.near_out = c->near_buf[1 - cur].p;
+        a.far_out = c->far_buf[fcur].p;
+        a.t_near = t_near;
+        a.bound = bound;
+        a.base = new_base;
+        {
+            const unsigned long long blocks = std::min<unsigned long long>(2048, (nn + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(partition_kernel, dim3((unsigned)std::max<unsigned long long>(blocks, 1)), dim3(kBlock), 0,
+                               c->stream, c->near_buf[cur].p, nn, t, bound, new_base, cfg.kmax, c->batch.p,
+                               c->near_buf[1 - cur].p, cfg.near_cap, st, st_next);
+            PA_TRY(check_launch());
+        }
+        const unsigned long long nb = std::min<unsigned long long>(sel, cfg.kmax);
+        if (nb > 0) {
+            const unsigned long long blocks =
+                std::min<unsigned long long>(4096, (nb + per_block - 1) / per_block);
+            if (cfg.profile)
+                HIP_TRY(hipEventRecord(c->ev0, c->stream));
+            ops.expand(dim3((unsigned)blocks), dim3(kBlock), c->stream, a);
+            PA_TRY(check_launch());
+            if (cfg.profile)
+                HIP_TRY(hipEventRecord(c->ev1, c->stream));
+            launches++;
+        }
+        if (G > 1) {
+            // exchange: counts, then records (grouped point-to-point over xGMI)
+            HIP_TRY(hipMemcpyAsync(c->h_stats, st, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            std::vector<unsigned long long> send(G), recv(G);
+            for (int d = 0; d < G; d++)
+                send[d] = std::min<unsigned long long>(c->h_stats->outbox_count[d], cfg.outbox_cap);
+            HIP_TRY(hipMemcpyAsync(c->xcounts.p, send.data(), 8 * G, hipMemcpyHostToDevice, c->stream));
+            NCCL_TRY(ncclGroupStart());
+            for (int d = 0; d < G; d++) {
+                NCCL_TRY(ncclSend(c->xcounts.p + d, 1, ncclUint64, d, c->comm, c->stream));
+                NCCL_TRY(ncclRecv(c->xcounts.p + G + d, 1, ncclUint64, d, c->comm, c->stream));
+            }
+            NCCL_TRY(ncclGroupEnd());
+            HIP_TRY(hipMemcpyAsync(recv.data(), c->xcounts.p + G, 8 * G, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            std::vector<unsigned long long> roff(G + 1, 0);
+            for (int d = 0; d < G; d++)
+                roff[d + 1] = roff[d] + recv[d];
+            NCCL_TRY(ncclGroupStart());
+            for (int d = 0; d < G; d++) {
+                if (d == c->shard)
+                    continue;
+                if (send[d])
+                    NCCL_TRY(ncclSend(c->outbox.p + (size_t)d * cfg.outbox_cap * rb, send[d] * rb, ncclUint8, d,
+                                      c->comm, c->stream));
+                if (recv[d])
+                    NCCL_TRY(ncclRecv(c->inbox.p + roff[d] * rb, recv[d] * rb, ncclUint8, d, c->comm, c->stream));
+            }
+            NCCL_TRY(ncclGroupEnd());
+            const unsigned long long total = roff[G];
+            for (int d = 0; d < G; d++)
+                if (d != c->shard)
+                    exchanged += (int64_t)send[d];
+            if (total) {
+                const unsigned long long blocks = std::min<unsigned long long>(4096, (total + kBlock - 1) / kBlock);
+                ops.insert_remote(dim3((unsigned)blocks), dim3(kBlock), c->stream, a, c->inbox.p, total);
+                PA_TRY(check_launch());
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(c->h_stats, st, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+        unsigned long long far_count = 0;
+        int goal_dev = kIntMax;
+        HIP_TRY(hipMemcpyAsync(&far_count, c->far_n.p, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&goal_dev, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (cfg.profile && nb > 0) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+            expand_ms += ms;
+        }
+        const StepStats &hs = *c->h_stats;
+        if (hs.overflow)
+            return fail(PASTAR_ENOMEM, "device capacity exhausted at step %lld (near %llu/%llu, far %llu/%llu, "
+                        "batch %llu, table 2^%d)", (long long)steps, hs.near_count, cfg.near_cap, far_count,
+                        cfg.far_cap, cfg.kmax, cfg.table_log2);
+        expanded += (int64_t)hs.expanded;
+        reopen += (int64_t)hs.reopen;
+        generated += (int64_t)hs.generated;
+        claimed += (int64_t)hs.claimed;
+        parents += (int64_t)nb;
+        cur = 1 - cur;
+        nn = hs.near_count;
+        nf = far_count;
+        base = new_base;
+        std::memcpy(hist.data(), hs.hist, sizeof(unsigned int) * kHistBins);
+        goal_g = goal_dev;
+        steps++;
+
+        // refill the near pile from the far pile (raise t_near)
+        if (nn < cfg.kmax && nf > 0) {
+            FarStats init{};
+            init.min_f = kIntMax;
+            HIP_TRY(hipMemcpyAsync(c->farstats.p, &init, sizeof(FarStats), hipMemcpyHostToDevice, c->stream));
+            const unsigned long long blocks = std::min<unsigned long long>(2048, (nf + kBlock - 1) / kBlock);
+            hipLaunchKernelGGL(far_min_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->far_buf[fcur].p, nf,
+                               goal_g, c->farstats.p);
+            PA_TRY(check_launch());
+            HIP_TRY(hipMemcpyAsync(c->h_far, c->farstats.p, sizeof(FarStats), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            const int far_min = c->h_far->min_f;
+            if (c->h_far->live == 0) {
+                nf = 0;
+                HIP_TRY(hipMemsetAsync(c->far_n.p, 0, 8, c->stream));
+            } else {
+                if (nn == 0) {
+                    base = far_min;
+                    std::fill(hist.begin(), hist.end(), 0u);
+                }
+                const int cap_t = base + kHistBins - 1;
+                if (far_min < cap_t) {
+                    hipLaunchKernelGGL(far_hist_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream,
+                                       c->far_buf[fcur].p, nf, goal_g, far_min, c->farstats.p);
+                    PA_TRY(check_launch());
+                    HIP_TRY(hipMemcpyAsync(c->h_far, c->farstats.p, sizeof(FarStats), hipMemcpyDeviceToHost, c->stream));
+                    HIP_TRY(hipStreamSynchronize(c->stream));
+                    // enough entries for several steps, within the histogram window
+                    const unsigned long long want = 4 * cfg.kmax;
+                    unsigned long long cum = 0;
+                    int tn = cap_t;
+                    for (int b = 0; b < kHistBins - 1; b++) {
+                        cum += c->h_far->hist[b];
+                        if (cum >= want) {
+                            tn = far_min + b + 1;
+                            break;
+                        }
+                    }
+                    tn = std::min(tn, cap_t);
+                    StepStats *rs = c->stats.p + 2;
+                    HIP_TRY(hipMemsetAsync(rs, 0, sizeof(StepStats), c->stream));
+                    hipLaunchKernelGGL(far_partition_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream,
+                                       c->far_buf[fcur].p, nf, tn, goal_g, base, c->near_buf[cur].p + nn,
+                                       cfg.near_cap - nn, c->far_buf[1 - fcur].p, cfg.far_cap, rs);
+                    PA_TRY(check_launch());
+                    HIP_TRY(hipMemcpyAsync(c->h_stats, rs, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+                    HIP_TRY(hipStreamSynchronize(c->stream));
+                    if (c->h_stats->overflow)
+                        return fail(PASTAR_ENOMEM, "near pile capacity exhausted during refill");
+                    nn += c->h_stats->near_count;
+                    nf = c->h_stats->far_count;
+                    for (int b = 0; b < kHistBins; b++)
+                        hist[b] += c->h_stats->hist[b];
+                    HIP_TRY(hipMemcpyAsync(c->far_n.p, &nf, 8, hipMemcpyHostToDevice, c->stream));
+                    fcur = 1 - fcur;
+                    t_near = tn;
+                }
+            }
+        }
+
+        // termination
+        if (G > 1) {
+            int64_t mn[1] = {goal_g};
+            PA_TRY(allreduce_i64(c, mn, 1, ncclMin));
+            goal_g = (int)mn[0];
+            HIP_TRY(hipMemcpyAsync(c->goal.p, &goal_g, 4, hipMemcpyHostToDevice, c->stream));
+            int64_t rem[1] = {(int64_t)(nn + nf)};
+            PA_TRY(allreduce_i64(c, rem, 1, ncclSum));
+            done = rem[0] == 0;
+        } else {
+            done = nn == 0 && nf == 0;
+        }
+        if (cfg.verbose && (steps % 100 == 0 || done))
+            std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %lld near %llu far %llu goal %d base %d t_near %d\n",
+                         c->shard, G, (long long)steps, (long long)expanded, nn, nf, goal_g, base, t_near);
+    }
+    const double t1 = now_s();
+    if (goal_g == kIntMax)
+        return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
+
+    // table census
+    DevBuf<unsigned long long> cnt;
+    PA_TRY(cnt.alloc(2));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 16, c->stream));
+    hipLaunchKernelGGL(count_table_kernel, dim3(2048), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
+                       slot_words_rt(c->kw), c->kw, cnt.p);
+    PA_TRY(check_launch());
+    unsigned long long census[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(census, cnt.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+
+    std::memset(res, 0, sizeof(*res));
+    res->score = goal_g;
+    res->expansions = expanded;
+    res->reopen = reopen;
+    res->generated = generated;
+    res->open_size = (int64_t)(nn + nf);
+    res->closed_size = (int64_t)census[1];
+    res->table_used = (int64_t)census[0];
+    res->steps = steps;
+    res->exchanged = exchanged;
+    res->seconds = t1 - t0;
+    res->expand_ms = expand_ms;
+    res->expand_launches = launches;
+    res->expand_parents = parents;
+    int64_t all[1] = {expanded};
+    if (G > 1)
+        PA_TRY(allreduce_i64(c, all, 1, ncclSum));
+    // the goal's acceptance counts as one expansion (PAStar.cpp:341)
+    res->expansions_all = all[0] + 1;
+    c->searched = true;
+    c->score = goal_g;
+    return PASTAR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_result *res)
+{
+    if (!c || !res)
+        return fail(PASTAR_EINVAL, "null argument");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    if (c->searched)
+        return fail(PASTAR_ESTATE, "context already searched; create a new context");
+    HIP_TRY(hipSetDevice(c->device));
+    pastar_search_opts o{};
+    if (opts)
+        o = *opts;
+    SearchCfg cfg;
+    const unsigned long long masks = (1ull << c->n) - 1;
+    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 8192ull;
+    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 24;
+    if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
+        return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
+    cfg.near_cap = o.near_capacity > 0 ? (unsigned long long)o.near_capacity
+                                       : std::max<unsigned long long>(1ull << 22, 2 * cfg.kmax * masks);
+    cfg.far_cap = o.far_capacity > 0 ? (unsigned long long)o.far_capacity : (1ull << 24);
+    cfg.outbox_cap = cfg.kmax * masks;
+    cfg.verbose = o.verbose;
+    cfg.profile = o.profile;
+    cfg.max_steps = o.max_steps;
+    int rc;
+    if (c->kw == 1)
+        rc = search_impl<1>(c, cfg, res);
+    else if (c->kw == 2)
+        rc = search_impl<2>(c, cfg, res);
+    else
+        rc = search_impl<4>(c, cfg, res);
+    return rc;
+}
+
+int pastar_gpu_closed_lookup(pastar_ctx *c, const uint16_t *pos, pastar_node *out)
+{
+    if (!c || !pos || !out)
+        return fail(PASTAR_EINVAL, "null argument");
+    if (!c->searched)
+        return fail(PASTAR_ESTATE, "no search has run on this context");
+    HIP_TRY(hipSetDevice(c->device));
+    uint64_t key[4];
+    pack_key(c, pos, key);
+    DevBuf<uint64_t> dk, dout;
+    PA_TRY(dk.alloc(4));
+    PA_TRY(dout.alloc(3));
+    HIP_TRY(hipMemcpyAsync(dk.p, key, 32, hipMemcpyHostToDevice, c->stream));
+    ops_for(c).lookup(c->stream, c->table.p, c->nslots - 1, dk.p, dout.p);
+    PA_TRY(check_launch());
+    uint64_t r[3];
+    HIP_TRY(hipMemcpyAsync(r, dout.p, 24, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!r[0])
+        return fail(PASTAR_ENOTFOUND, "coordinate not in the node table of shard %d", c->shard);
+    std::memset(out, 0, sizeof(*out));
+    std::memcpy(out->pos, pos, sizeof(uint16_t) * c->n);
+    out->g = (int32_t)(r[1] >> 32);
+    out->parent_mask = (int32_t)(uint32_t)r[1];
+    out->f = out->g + (int32_t)(r[2] >> 32);
+    return PASTAR_OK;
+}
+
+int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
+{
+    if (!c || !rows || !cols)
+        return fail(PASTAR_EINVAL, "null argument");
+    if (!c->searched)
+        return fail(PASTAR_ESTATE, "no search has run on this context");
+    HIP_TRY(hipSetDevice(c->device));
+    int total_len = 0;
+    for (int i = 0; i < c->n; i++)
+        total_len += c->hp.len[i];
+    if (stride < total_len + 1)
+        return fail(PASTAR_EINVAL, "stride %d < %d", stride, total_len + 1);
+    const Ops ops = ops_for(c);
+    DevBuf<uint64_t> dkey, dlast;
+    DevBuf<int32_t> dmasks;
+    DevBuf<int> dinfo;
+    PA_TRY(dkey.alloc(4));
+    PA_TRY(dlast.alloc(4));
+    PA_TRY(dmasks.alloc((size_t)total_len + 1));
+    PA_TRY(dinfo.alloc(2));
+    // walk from the goal towards the origin; with several shards the walk
+    // hops to the owner of each parent (PAStarDistributedBacktrace.cpp:19-213)
+    std::vector<uint16_t> pos(PASTAR_MAX_SEQ, 0);
+    for (int i = 0; i < c->n; i++)
+        pos[i] = (uint16_t)c->hp.len[i];
+    std::vector<int32_t> path;  // masks from the goal backwards
+    const int G = c->n_shards;
+    for (int guard = 0; guard <= total_len + 1; guard++) {
+        bool origin = true;
+        for (int i = 0; i < c->n; i++)
+            origin &= pos[i] == 0;
+        if (origin)
+            break;
+        const int owner = G > 1 ? owner_of(c->n, pos.data(), G, c->hp.hash_type, c->hp.hash_shift) : 0;
+        int info[2] = {0, 0};
+        std::vector<int32_t> seg;
+        if (owner == c->shard) {
+            uint64_t key[4];
+            pack_key(c, pos.data(), key);
+            HIP_TRY(hipMemcpyAsync(dkey.p, key, 32, hipMemcpyHostToDevice, c->stream));
+            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, dkey.p, total_len + 1, G > 1 ? 1 : 0, dmasks.p,
+                     dlast.p, dinfo.p);
+            PA_TRY(check_launch());
+            HIP_TRY(hipMemcpyAsync(info, dinfo.p, 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (info[1] < 0 || info[1] == 2)
+                return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d)", info[0], info[1]);
+        }
+        if (G > 1) {
+            NCCL_TRY(ncclBroadcast(dinfo.p, dinfo.p, 2, ncclInt32, owner, c->comm, c->stream));
+            HIP_TRY(hipMemcpyAsync(info, dinfo.p, 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (info[1] < 0 || info[1] == 2)
+                return fail(PASTAR_ENOTFOUND, "backtrace broken on shard %d", owner);
+            if (info[0] > 0)
+                NCCL_TRY(ncclBroadcast(dmasks.p, dmasks.p, (size_t)info[0], ncclInt32, owner, c->comm, c->stream));
+        }
+        seg.resize((size_t)info[0]);
+        if (info[0] > 0)
+            HIP_TRY(hipMemcpyAsync(seg.data(), dmasks.p, 4 * (size_t)info[0], hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int32_t m : seg) {
+            path.push_back(m);
+            for (int i = 0; i < c->n; i++)
+                pos[i] = (uint16_t)(pos[i] - ((m >> i) & 1));
+        }
+        if (info[0] == 0)
+            return fail(PASTAR_ENOTFOUND, "backtrace made no progress");
+    }
+    const int L = (int)path.size();
+    std::vector<int> at(c->n, 0);
+    for (int k = 0; k < L; k++) {
+        const int32_t m = path[(size_t)(L - 1 - k)];
+        for (int i = 0; i < c->n; i++) {
+            if ((m >> i) & 1)
+                rows[(size_t)i * stride + k] = c->seqs[i][at[i]++];
+            else
+                rows[(size_t)i * stride + k] = '-';
+        }
+    }
+    for (int i = 0; i < c->n; i++)
+        rows[(size_t)i * stride + L] = '\0';
+    *cols = L;
+    return PASTAR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+"""Python mirror of the reference's PAStar hot-path interface, over the C-ABI.
+
+Reference names kept (Gabrielcarvfer/mpi_pastar_msa, paths relative to its
+root):
+
+  Sequences            pastar/include/Sequences.h:15-39  (object, not singleton)
+  Node                 pastar/include/Node.h:23-66
+  HeuristicHPair       pastar/include/HeuristicHPair.h:15-29 -> Engine.init(),
+                       Engine.calculate_h(), Engine.weight_matrix
+  Node.getNeigh        pastar/Node.cpp:206-248 -> Engine.get_neigh()
+  Coord.get_id         pastar/CoordHash.cpp:191-245 -> get_id()
+  PAStarOpt            pastar/include/PAStar.h:87-112
+  PAStar.pa_star       pastar/PAStar.cpp:627-673 -> Engine.pa_star()
+
+Errors follow the reference: an invalid hash shift or thread count raises
+ValueError (std::invalid_argument there); a missing FASTA file raises
+OSError ("Can't open file", read_fasta.cpp:17-20).
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as nat
+from ._native import check, lib
+
+MAX_SEQ = nat.MAX_SEQ
+GAP_OPEN = GAP_EXTENSION = GAP_GAP = 30  # Cost.h:13
+
+
+def cost(r, l):
+    """Cost::cost (Cost.cpp:266-270)."""
+    return lib().pastar_cost(ord(r) if isinstance(r, str) else r, ord(l) if isinstance(l, str) else l)
+
+
+def get_id(coord, size, hash_type="FZORDER", hash_shift=12):
+    """Coord<N>::get_id: owner of a coordinate among `size` workers/shards."""
+    if not 0 <= hash_shift <= 21:
+        raise ValueError("Invalid Hash Shift")
+    ht = nat.HASH_TYPES[hash_type] if isinstance(hash_type, str) else int(hash_type)
+    c = (ctypes.c_uint16 * MAX_SEQ)(*coord)
+    return lib().pastar_owner(len(coord), c, int(size), ht, int(hash_shift))
+
+
+class Sequences:
+    """The sequences being aligned (Sequences.cpp:53-87)."""
+
+    def __init__(self, seqs):
+        self.seqs = [s if isinstance(s, str) else s.decode() for s in seqs]
+        if not 2 <= len(self.seqs) <= MAX_SEQ:
+            raise ValueError("Invalid number of sequences: %d" % len(self.seqs))
+
+    @classmethod
+    def from_fasta(cls, path):
+        """read_fasta_file (read_fasta.cpp:8-56), quirks included."""
+        n = ctypes.c_int(MAX_SEQ)
+        lengths = (ctypes.c_int * MAX_SEQ)()
+        cap = 1 << 22
+        buf = ctypes.create_string_buffer(cap)
+        rc = lib().pastar_read_fasta(str(path).encode(), buf, cap, ctypes.byref(n), lengths)
+        if rc == nat.EIO:
+            raise OSError("Can't open file %s" % path)
+        check(rc)
+        seqs, off = [], 0
+        for i in range(n.value):
+            seqs.append(buf.raw[off:off + lengths[i]].decode("latin-1"))
+            off += lengths[i]
+        return cls(seqs)
+
+    def get_seq(self, i):
+        return self.seqs[i]
+
+    def get_seq_num(self):
+        return len(self.seqs)
+
+    def get_final_coord(self):
+        return tuple(len(s) for s in self.seqs)
+
+    def get_initial_coord(self):
+        return tuple(0 for _ in self.seqs)
+
+    def get_initial_node(self):
+        """Origin with parenti = (1 << N) - 1 (Sequences.cpp:70-77); f is filled by the engine."""
+        return Node(self.get_initial_coord(), 0, 0, (1 << len(self.seqs)) - 1)
+
+
+@dataclass
+class Node:
+    pos: tuple
+    g: int
+    f: int
+    parenti: int
+
+    def get_g(self):
+        return self.g
+
+    def get_f(self):
+        return self.f
+
+    def get_h(self):
+        return self.f - self.g
+
+    def get_parenti(self):
+        return self.parenti
+
+    def get_parent(self):
+        return tuple(c - ((self.parenti >> i) & 1) for i, c in enumerate(self.pos))
+
+    def __str__(self):  # Node.cpp:41-47
+        return "(%s)\tg - %d (h - %d f - %d)" % (" ".join(map(str, self.pos)), self.g, self.get_h(), self.f)
+
+
+@dataclass
+class PAStarOpt:
+    """PAStarOpt (PAStar.h:87-112) plus the device-search knobs."""
+    hash_type: str = "FZORDER"
+    hash_shift: int = 12
+    threads_num: int = 1
+    batch_nodes: int = 0
+    table_slots_log2: int = 0
+    near_capacity: int = 0
+    far_capacity: int = 0
+    max_steps: int = 0
+    profile: bool = False
+    verbose: bool = False
+
+    def search_opts(self):
+        return nat.pastar_search_opts(self.batch_nodes, self.table_slots_log2, self.near_capacity,
+                                      self.far_capacity, self.max_steps, int(self.profile), int(self.verbose))
+
+
+def compute_weights(seqs):
+    """weightAltschulsRationale2 on the host (float n x n matrix)."""
+    n = len(seqs)
+    arr = (ctypes.c_char_p * n)(*[s.encode("latin-1") for s in seqs])
+    lens = (ctypes.c_int * n)(*[len(s) for s in seqs])
+    out = (ctypes.c_float * (n * n))()
+    check(lib().pastar_compute_weights(n, arr, lens, out))
+    return np.array(out[:], dtype=np.float32).reshape(n, n)
+
+
+def rccl_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    check(lib().pastar_rccl_unique_id(buf))
+    return buf.raw
+
+
+@dataclass
+class SearchResult:
+    score: int
+    expansions: int
+    expansions_all: int
+    reopen: int
+    generated: int
+    open_size: int
+    closed_size: int
+    table_used: int
+    steps: int
+    exchanged: int
+    seconds: float
+    expand_ms: float
+    expand_launches: int
+    expand_parents: int
+    extra: dict = field(default_factory=dict)
+
+
+class Engine:
+    """One device context (one GPU shard).  Owns the device memory."""
+
+    def __init__(self, sequences, device=0, n_shards=1, shard_rank=0, rccl_id=None, weights=None,
+                 hash_type="FZORDER", hash_shift=12, gap_open=GAP_OPEN, gap_ext=GAP_EXTENSION,
+                 gap_gap=GAP_GAP):
+        if isinstance(sequences, (list, tuple)):
+            sequences = Sequences(sequences)
+        if not 0 <= hash_shift <= 21:
+            raise ValueError("Invalid Hash Shift")
+        self.sequences = sequences
+        seqs = sequences.seqs
+        self.n = len(seqs)
+        self.n_shards = n_shards
+        self.shard_rank = shard_rank
+        self._keep = [s.encode("latin-1") for s in seqs]
+        self._lens = (ctypes.c_int * self.n)(*[len(s) for s in seqs])
+        self._res = (ctypes.c_char_p * self.n)(*self._keep)
+        npairs = self.n * (self.n - 1) // 2
+        self._w = (ctypes.c_int * npairs)(*weights) if weights is not None else None
+        ht = nat.HASH_TYPES[hash_type] if isinstance(hash_type, str) else int(hash_type)
+        self.hash_type, self.hash_shift = ht, hash_shift
+        prob = nat.pastar_problem(self.n, self._lens, self._res,
+                                  self._w if self._w is not None else None, None,
+                                  gap_open, gap_ext, gap_gap, ht, hash_shift)
+        self._ctx = ctypes.c_void_p()
+        check(lib().pastar_gpu_create(ctypes.byref(prob), device, n_shards, shard_rank, rccl_id,
+                                      ctypes.byref(self._ctx)))
+        self.npairs = npairs
+        self.pairs = [(x, y) for x in range(self.n - 1) for y in range(x + 1, self.n)]
+        self._ready = False
+
+    def close(self):
+        if self._ctx:
+            lib().pastar_gpu_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- HeuristicHPair ----
+    def init(self):
+        """HeuristicHPair::init: PairAlign tables on the GPU (wavefront kernel)."""
+        check(lib().pastar_gpu_build_heuristic(self._ctx))
+        self._ready = True
+        return self
+
+    @property
+    def weight_matrix(self):
+        """(int)weightMatrix[x][y] for the pairs in row-major order."""
+        out = (ctypes.c_int32 * self.npairs)()
+        check(lib().pastar_gpu_weights(self._ctx, out))
+        return list(out)
+
+    def pair_table(self, k):
+        """PairAlign k's full suffix table as an (L_x+1, L_y+1) int32 array."""
+        x, y = self.pairs[k]
+        lx, ly = len(self.sequences.seqs[x]), len(self.sequences.seqs[y])
+        out = np.empty((lx + 1) * (ly + 1), dtype=np.int32)
+        check(lib().pastar_gpu_pair_table(self._ctx, k, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out.reshape(lx + 1, ly + 1)
+
+    def calculate_h(self, coords):
+        """HeuristicHPair::calculate_h for one coordinate or an (m, n) array."""
+        arr = np.asarray(coords, dtype=np.uint16)
+        single = arr.ndim == 1
+        arr = np.atleast_2d(arr)
+        buf = np.zeros((arr.shape[0], MAX_SEQ), dtype=np.uint16)
+        buf[:, :self.n] = arr
+        out = np.empty(arr.shape[0], dtype=np.int32)
+        check(lib().pastar_gpu_h(self._ctx, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), arr.shape[0],
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return int(out[0]) if single else out
+
+    # ---- Node::getNeigh ----
+    def get_neigh_batch(self, nodes, vec_size=1):
+        """Batched getNeigh: returns (children, owner, src) for a list of Node."""
+        n_in = len(nodes)
+        arr = (nat.pastar_node * max(n_in, 1))()
+        for k, nd in enumerate(nodes):
+            for i, c in enumerate(nd.pos):
+                arr[k].pos[i] = c
+            arr[k].g, arr[k].f, arr[k].parent_mask = nd.g, nd.f, nd.parenti
+        cap = max(n_in * ((1 << self.n) - 1), 1)
+        out = (nat.pastar_node * cap)()
+        own = (ctypes.c_int32 * cap)()
+        src = (ctypes.c_int32 * cap)()
+        cnt = ctypes.c_int64()
+        check(lib().pastar_gpu_expand(self._ctx, arr, n_in, vec_size, out, own, src, ctypes.byref(cnt)))
+        kids = [Node(tuple(out[k].pos[:self.n]), out[k].g, out[k].f, out[k].parent_mask)
+                for k in range(cnt.value)]
+        return kids, list(own[:cnt.value]), list(src[:cnt.value])
+
+    def get_neigh(self, node, vec_size=1):
+        """Node::getNeigh(a, vec_size): neighbours bucketed by owner, mask order kept."""
+        kids, owner, _ = self.get_neigh_batch([node], vec_size)
+        a = [[] for _ in range(vec_size)]
+        for k, o in zip(kids, owner):
+            a[o].append(k)
+        return a
+
+    def initial_node(self):
+        nd = self.sequences.get_initial_node()
+        nd.f = self.calculate_h(nd.pos)
+        return nd
+
+    # ---- PAStar ----
+    def pa_star(self, opt=None):
+        """Run the device-resident search to the optimal alignment."""
+        opt = opt or PAStarOpt()
+        if opt.threads_num <= 0:
+            raise ValueError("Invalid number of threads")
+        if not self._ready:
+            self.init()
+        r = nat.pastar_result()
+        so = opt.search_opts()
+        check(lib().pastar_gpu_search(self._ctx, ctypes.byref(so), ctypes.byref(r)))
+        return SearchResult(**r.as_dict())
+
+    def closed_lookup(self, coord):
+        c = (ctypes.c_uint16 * MAX_SEQ)(*coord)
+        out = nat.pastar_node()
+        rc = lib().pastar_gpu_closed_lookup(self._ctx, c, ctypes.byref(out))
+        if rc == nat.ENOTFOUND:
+            return None
+        check(rc)
+        return Node(tuple(out.pos[:self.n]), out.g, out.f, out.parent_mask)
+
+    def alignment(self):
+        """Backtrace rows (collective over shards)."""
+        stride = sum(len(s) for s in self.sequences.seqs) + 1
+        buf = ctypes.create_string_buffer(self.n * stride)
+        cols = ctypes.c_int()
+        check(lib().pastar_gpu_alignment(self._ctx, buf, stride, ctypes.byref(cols)))
+        raw = buf.raw
+        return [raw[i * stride:i * stride + cols.value].decode("latin-1") for i in range(self.n)]
+
+
+def similarity(rows):
+    """backtrace_print_similarity (backtrace.cpp:136-165): percent as a float32."""
+    n, total, equal = len(rows), 0, 0
+    for col in zip(*rows):
+        for i in range(n):
+            for j in range(i + 1, n):
+                equal += col[i] == col[j]
+                total += 1
+    return float(np.float32(equal * 100) / np.float32(total))

@@ -1,0 +1,141 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle and
+the reference's known-answer values.  Integer work: every comparison is exact.
+"""
+import hashlib
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_bind as orc
+from conftest import golden
+from mpi_pastar_msa_amd import Engine, PAStarOpt, Sequences, similarity
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["test", "test2", "PF08184", "syn4x200_s1"]
+
+
+def _engine(name, kat, **kw):
+    seqs = Sequences.from_fasta(golden(kat["inputs"][name]["file"]))
+    return Engine(seqs, **kw).init()
+
+
+@pytest.fixture(scope="module")
+def oracles(kat):
+    return {k: orc.Oracle(fasta=golden(kat["inputs"][k]["file"])) for k in SMALL + ["kinase"]}
+
+
+@pytest.mark.parametrize("name", SMALL + ["kinase"])
+def test_pairalign_tables_bit_exact(name, kat, oracles):
+    o = oracles[name]
+    with _engine(name, kat) as e:
+        assert e.weight_matrix == o.weights
+        for k in range(e.npairs):
+            np.testing.assert_array_equal(e.pair_table(k), o.pair_table(k))
+
+
+@pytest.mark.parametrize("name", SMALL + ["kinase"])
+def test_h_origin_and_first_expansion(name, kat, oracles):
+    ref = kat["inputs"][name]
+    with _engine(name, kat) as e:
+        node = e.initial_node()
+        assert node.f == ref["h_origin"]
+        kids = e.get_neigh(node)[0]
+        fe = ref["first_expansion"]
+        assert len(kids) == fe["count"]
+        assert sum(k.g for k in kids) == fe["sum_g"]
+        assert sum(k.get_h() for k in kids) == fe["sum_h"]
+        assert [kids[0].g, kids[0].get_h()] == fe["first"]
+        assert [kids[-1].g, kids[-1].get_h()] == fe["last"]
+        assert [k.parenti for k in kids] == list(range(1, len(kids) + 1))
+
+
+def _random_nodes(o, count, rng):
+    nodes = []
+    for _ in range(count):
+        pos = tuple(rng.randint(0, L) for L in o.lengths)
+        if rng.random() < 0.2:  # border nodes: some coordinates at their end
+            pos = tuple(L if rng.random() < 0.5 else c for c, L in zip(pos, o.lengths))
+        parenti = rng.randint(1, (1 << o.n) - 1)
+        g = rng.randint(0, 10 ** 6)
+        nodes.append((pos, g, g + o.h(pos), parenti))
+    return nodes
+
+
+@pytest.mark.parametrize("name", SMALL + ["kinase"])
+@pytest.mark.parametrize("vec_size,hash_type,shift", [(1, 0, 12), (8, 0, 12), (64, 0, 12), (7, 0, 3),
+                                                      (16, 1, 5), (8, 2, 2), (8, 3, 0), (5, 0, 0)])
+def test_get_neigh_matches_oracle(name, vec_size, hash_type, shift, kat, oracles):
+    o = oracles[name]
+    rng = random.Random(zlib.crc32(("%s/%d/%d/%d" % (name, vec_size, hash_type, shift)).encode()))
+    nodes = _random_nodes(o, 200, rng)
+    seqs = Sequences.from_fasta(golden(kat["inputs"][name]["file"]))
+    with Engine(seqs, hash_type=hash_type, hash_shift=shift).init() as e:
+        from mpi_pastar_msa_amd.pastar import Node
+        kids, owner, src = e.get_neigh_batch([Node(*nd) for nd in nodes], vec_size)
+        got = {}
+        for k, ow, s in zip(kids, owner, src):
+            got.setdefault(s, []).append(((k.pos, k.g, k.f, k.parenti), ow))
+        for s, nd in enumerate(nodes):
+            assert got.get(s, []) == o.get_neigh(nd, vec_size, hash_type, shift), (s, nd)
+
+
+@pytest.mark.parametrize("name", SMALL)
+@pytest.mark.parametrize("batch", [0, 1, 64])
+def test_search_score_bit_exact(name, batch, kat, oracles):
+    ref = kat["inputs"][name]
+    with _engine(name, kat) as e:
+        r = e.pa_star(PAStarOpt(batch_nodes=batch))
+        assert r.score == ref["score"]
+        rows = e.alignment()
+        # the backtrace is a real alignment whose SP cost is the score
+        assert [row.replace("-", "") for row in rows] == e.sequences.seqs
+        assert oracles[name].alignment_cost(rows) == ref["score"]
+        if "alignment_md5" in ref:
+            assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+        assert "%.2f" % similarity(rows) == ref["similarity"]
+        # a goal with f == score is in the closed list
+        goal = e.closed_lookup(e.sequences.get_final_coord())
+        assert goal is not None and goal.g == ref["score"]
+        if batch == 1:  # one node per step = serial A* order up to ties
+            assert r.expansions_all >= ref["expansions_t1"]
+
+
+def test_search_kinase(kat, oracles):
+    ref = kat["inputs"]["kinase"]
+    with _engine("kinase", kat) as e:
+        r = e.pa_star(PAStarOpt(table_slots_log2=26, far_capacity=1 << 26))
+        assert r.score == ref["score"]
+        rows = e.alignment()
+        assert oracles["kinase"].alignment_cost(rows) == ref["score"]
+        assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
+@pytest.mark.parametrize("name", ["syn8x400_s11", "syn8x100_s3"])
+def test_search_n8(name, kat):
+    ref = kat["inputs"][name]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    with Engine(seqs).init() as e:
+        r = e.pa_star(PAStarOpt(table_slots_log2=27, far_capacity=1 << 27))
+        assert r.score == ref["score"]
+        rows = e.alignment()
+        assert o.alignment_cost(rows) == ref["score"]
+
+
+def test_random_small_problems_match_oracle():
+    rng = random.Random(7)
+    alphabet = "ACDEFGHIKLMNPQRSTVWYBZ"
+    for trial in range(12):
+        n = rng.randint(3, 6)
+        seqs = ["".join(rng.choice(alphabet[:20 + trial % 4]) for _ in range(rng.randint(1, 14))) for _ in range(n)]
+        o = orc.Oracle(seqs=seqs)
+        ref = o.astar()
+        with Engine(seqs).init() as e:
+            assert e.weight_matrix == o.weights
+            r = e.pa_star(PAStarOpt(batch_nodes=rng.choice([1, 3, 16, 0])))
+            assert r.score == ref["score"], (seqs, r, ref)
+            rows = e.alignment()
+            assert o.alignment_cost(rows) == ref["score"]
