@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X PAStar engine (BASELINE.json metric).
+
+One *step* = one full search of the workload on the GPU(s): PairAlign
+precompute (wavefront kernel), the batched device-resident A* to the optimal
+SP score, and the backtrace of the alignment.  The sequences are synthetic
+(tools/gen_synthetic.py) and uploaded before the timed
+region; contexts and device buffers are created before it too.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+N > 1 runs one rank per GPU (torch.distributed.run); the ranks shard one
+search by the reference's z-order owner hash and exchange nodes over RCCL
+(strong scaling: the total work is one search).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "A* nodes expanded/sec + wall-clock to optimal SP alignment, 1/2/4/8 MI355X"
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+WORKLOADS = {  # name -> (fasta fixture, BASELINE.json config it stands for, known optimal score)
+    "syn4x200_s1": ("syn4x200_s1.fasta", "configs[1]: 4 synthetic seqs x200 residues", 149875),
+    "PF08184": ("PF08184.fasta", "configs[2]: PF08184.fasta", 24450),
+    "kinase": ("kinase.fasta", "configs[3]: kinase.fasta", 421546),
+    "syn8x400_s5": ("syn8x400_s5.fasta", "configs[4]: 8 synthetic seqs x400 residues", 1318889),
+    "syn8x100_s3": ("syn8x100_s3.fasta", "survey point: 8 synthetic seqs x100 residues", 703569),
+}
+# serial (-t 1) expansion counts of the reference, for the useful rate
+SERIAL_EXPANSIONS = {"syn4x200_s1": 22089, "PF08184": 60, "kinase": 4497279}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def bytes_per_expansion(n):
+    """Algorithmic HBM bytes of one expansion:
+    B_exp = S + 16P + N + 2MS, S = 2N + 12 (parent record, 4 H cells per pair,
+    residues, neighbour records written + one table probe each)."""
+    s = 2 * n + 12
+    p = n * (n - 1) // 2
+    m = (1 << n) - 1
+    return s + 16 * p + n + 2 * m * s
+
+
+def env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def cpu_baseline(fasta, budget_s):
+    """The oracle's serial PAStar (-t 1 restatement, 1 core) on the same input,
+    repeated until about `budget_s` seconds of CPU work (bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind  # test infrastructure: the CPU baseline leg only
+    o = oracle_bind.Oracle(fasta=fasta)
+    runs, exp, secs = 0, 0, 0.0
+    t_start = time.perf_counter()
+    while True:
+        r = o.astar()
+        runs += 1
+        exp += r["expansions"]
+        secs += r["seconds"]
+        if time.perf_counter() - t_start >= budget_s or runs >= 10000:
+            break
+    return {"value": exp / secs, "unit": "nodes/s", "cores": 1, "kind": "port",
+            "sample": "%d full serial searches of the workload (%d expansions each, %.2f s of search)"
+                      % (runs, exp // runs, secs),
+            "wall_to_optimal_s": secs / runs, "score": r["score"]}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per expand launch from a committed rocprofv3 PMC summary of
+    the same workload (profiles/pmc_<workload>.json, tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="syn4x200_s1", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="batch_nodes (0 = engine default)")
+    ap.add_argument("--table-log2", type=int, default=0)
+    ap.add_argument("--far-capacity", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = env_int("WORLD_SIZE", 1)
+    rank = env_int("RANK", 0)
+    local_rank = env_int("LOCAL_RANK", 0)
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
+        args.gpus = world
+
+    import torch
+    import torch.distributed as dist
+    from mpi_pastar_msa_amd import Engine, PAStarOpt, Sequences, rccl_unique_id
+
+    dist_on = world > 1
+    if dist_on:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    rid = None
+    if dist_on:
+        box = [rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        rid = box[0]
+
+    fasta_name, cfg_desc, known = WORKLOADS[args.workload]
+    fasta = os.path.join(GOLDEN, fasta_name)
+    seqs = Sequences.from_fasta(fasta)
+    n = len(seqs.seqs)
+    engine = Engine(seqs, device=local_rank, n_shards=world, shard_rank=rank, rccl_id=rid)
+    opt = PAStarOpt(batch_nodes=args.batch, table_slots_log2=args.table_log2,
+                    far_capacity=args.far_capacity, profile=True)
+
+    def step():
+        engine.init()
+        r = engine.pa_star(opt)
+        rows = engine.alignment()
+        return r, rows
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+
+    results = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        results.append(step())
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    exp_all = sum(r.expansions_all for r, _ in results)
+    exp_local = sum(r.expansions for r, _ in results)
+    kern_ms = sum(r.expand_ms for r, _ in results)
+    launches = sum(r.expand_launches for r, _ in results)
+    wall = sum(r.seconds for r, _ in results) / len(results)
+    score = results[-1][0].score
+    if dist_on:
+        t = torch.tensor([elapsed, wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, wall = float(t[0]), float(t[1])
+        # the roofline is reported for rank 0's expand kernel
+    if rank != 0:
+        if dist_on:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = exp_all / elapsed
+    b_exp = bytes_per_expansion(n)
+    avg_launch_s = (kern_ms / 1e3) / max(launches, 1)
+    achieved = (exp_local / max(launches, 1)) * b_exp / avg_launch_s / 1e9 if launches else 0.0
+    traffic, traffic_src = pmc_traffic(args.workload)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (tools/gen_synthetic.py, SURVEY.md §8(d)-gen)" if args.workload.startswith("syn")
+                else "reference fixture %s" % fasta_name,
+        "config": {"workload": args.workload, "baseline_config": cfg_desc, "n_seqs": n,
+                   "lengths": [len(s) for s in seqs.seqs], "hash": "FZORDER/12",
+                   "batch_nodes": args.batch or 8192, "parallelism": "shard%d" % world},
+        "score": score,
+        "score_ok": score == known,
+        "wall_to_optimal_s": wall,
+        "expansions_per_search": exp_all / args.steps,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "expand_kernel", "bytes_per_expansion": b_exp,
+                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
+                     "traffic_source": traffic_src},
+    }
+    if args.workload in SERIAL_EXPANSIONS:
+        line["useful_rate"] = SERIAL_EXPANSIONS[args.workload] / wall
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(fasta, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

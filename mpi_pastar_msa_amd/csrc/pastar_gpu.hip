@@ -136,6 +136,9 @@ struct pastar_ctx {
     FarStats *h_far = nullptr;            // pinned
     bool searched = false;
     int64_t score = -1;
+    // capacities of the current search buffers (reused across searches)
+    unsigned long long cap_kmax = 0, cap_near = 0, cap_far = 0, cap_outbox = 0;
+    int cap_log2 = 0;
 };
 
 namespace {
@@ -608,22 +611,32 @@ struct SearchCfg {
 int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
 {
     const int sw = slot_words_rt(c->kw);
-    c->nslots = 1ull << cfg.table_log2;
-    PA_TRY(c->table.alloc((size_t)c->nslots * sw));
-    PA_TRY(c->near_buf[0].alloc(cfg.near_cap));
-    PA_TRY(c->near_buf[1].alloc(cfg.near_cap));
-    PA_TRY(c->far_buf[0].alloc(cfg.far_cap));
-    PA_TRY(c->far_buf[1].alloc(cfg.far_cap));
-    PA_TRY(c->batch.alloc(cfg.kmax));
-    PA_TRY(c->stats.alloc(3));
-    PA_TRY(c->farstats.alloc(1));
-    PA_TRY(c->far_n.alloc(1));
-    PA_TRY(c->goal.alloc(1));
-    if (c->n_shards > 1) {
-        const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
-        PA_TRY(c->outbox.alloc(bytes));
-        PA_TRY(c->inbox.alloc(bytes));
-        PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
+    const bool same = c->table.p && c->cap_log2 == cfg.table_log2 && c->cap_kmax == cfg.kmax &&
+                      c->cap_near == cfg.near_cap && c->cap_far == cfg.far_cap && c->cap_outbox == cfg.outbox_cap;
+    if (!same) {
+        c->table.reset();  // free before allocating the next set
+        c->nslots = 1ull << cfg.table_log2;
+        PA_TRY(c->table.alloc((size_t)c->nslots * sw));
+        PA_TRY(c->near_buf[0].alloc(cfg.near_cap));
+        PA_TRY(c->near_buf[1].alloc(cfg.near_cap));
+        PA_TRY(c->far_buf[0].alloc(cfg.far_cap));
+        PA_TRY(c->far_buf[1].alloc(cfg.far_cap));
+        PA_TRY(c->batch.alloc(cfg.kmax));
+        PA_TRY(c->stats.alloc(3));
+        PA_TRY(c->farstats.alloc(1));
+        PA_TRY(c->far_n.alloc(1));
+        PA_TRY(c->goal.alloc(1));
+        if (c->n_shards > 1) {
+            const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
+            PA_TRY(c->outbox.alloc(bytes));
+            PA_TRY(c->inbox.alloc(bytes));
+            PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
+        }
+        c->cap_log2 = cfg.table_log2;
+        c->cap_kmax = cfg.kmax;
+        c->cap_near = cfg.near_cap;
+        c->cap_far = cfg.far_cap;
+        c->cap_outbox = cfg.outbox_cap;
     }
     const int blocks = (int)std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock);
     if (sw == 4)
@@ -633,8 +646,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     PA_TRY(check_launch());
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats) * 3, c->stream));
     HIP_TRY(hipMemsetAsync(c->far_n.p, 0, sizeof(unsigned long long), c->stream));
-    const int inf = kIntMax;
-    HIP_TRY(hipMemcpyAsync(c->goal.p, &inf, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
     return PASTAR_OK;
 }
 
@@ -980,8 +992,6 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         return fail(PASTAR_EINVAL, "null argument");
     if (!c->heuristic_ready)
         return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
-    if (c->searched)
-        return fail(PASTAR_ESTATE, "context already searched; create a new context");
     HIP_TRY(hipSetDevice(c->device));
     pastar_search_opts o{};
     if (opts)
