@@ -91,7 +91,8 @@ def main():
     ap.add_argument("--workload", default="syn4x200_s1", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="batch_nodes (0 = engine default)")
     ap.add_argument("--table-log2", type=int, default=0)
-    ap.add_argument("--far-capacity", type=int, default=0)
+    ap.add_argument("--pool", type=int, default=0, help="open-list entry pool (0 = engine default)")
+    ap.add_argument("--band", type=int, default=0, help="f band of one step (0 = engine default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -123,7 +124,7 @@ def main():
     n = len(seqs.seqs)
     engine = Engine(seqs, device=local_rank, n_shards=world, shard_rank=rank, rccl_id=rid)
     opt = PAStarOpt(batch_nodes=args.batch, table_slots_log2=args.table_log2,
-                    far_capacity=args.far_capacity, profile=True)
+                    pool_entries=args.pool, band=args.band, profile=True)
 
     def step():
         engine.init()
@@ -186,11 +187,13 @@ def main():
                 else "reference fixture %s" % fasta_name,
         "config": {"workload": args.workload, "baseline_config": cfg_desc, "n_seqs": n,
                    "lengths": [len(s) for s in seqs.seqs], "hash": "FZORDER/12",
-                   "batch_nodes": args.batch or 8192, "parallelism": "shard%d" % world},
+                   "batch_nodes": args.batch or 32768, "parallelism": "shard%d" % world},
         "score": score,
         "score_ok": score == known,
         "wall_to_optimal_s": wall,
         "expansions_per_search": exp_all / args.steps,
+        "steps_per_search": sum(r.steps for r, _ in results) / len(results),
+        "graph_replay": bool(results[-1][0].graph_replay),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "expand_kernel", "bytes_per_expansion": b_exp,

@@ -90,11 +90,19 @@ typedef struct pastar_node {
 typedef struct pastar_search_opts {
     int64_t batch_nodes;      /* target open nodes expanded per step        */
     int64_t table_slots_log2; /* open+closed hash table capacity (log2)     */
-    int64_t near_capacity;    /* entries of the near (f-window) open pile   */
-    int64_t far_capacity;     /* entries of the far open pile               */
+    int64_t pool_entries;     /* open-list entry pool (all f buckets)       */
+    int64_t subqueue_entries; /* entries one bucket sub-queue can hold      */
     int64_t max_steps;        /* safety stop (0 = unlimited)                */
+    int64_t band;             /* a step expands open nodes with f below the
+                                 current minimum + band (0 = auto: half the
+                                 mean f increase of one expansion)         */
     int32_t profile;          /* 1: time the expand kernel with HIP events  */
     int32_t verbose;
+    int32_t no_autogrow;      /* 1: fail with PASTAR_ENOMEM instead of
+                                 growing an exhausted capacity x4 and
+                                 restarting the search                     */
+    int32_t eager;            /* 1: launch every step from the host instead
+                                 of replaying a captured hipGraph          */
 } pastar_search_opts;
 
 typedef struct pastar_result {
@@ -112,6 +120,10 @@ typedef struct pastar_result {
     double expand_ms;       /* sum of expand-kernel durations (profile = 1)   */
     int64_t expand_launches;
     int64_t expand_parents; /* parents handed to the expand kernel            */
+    int64_t capacity_retries; /* restarts after growing an exhausted capacity */
+    int64_t table_slots;    /* node table capacity used                       */
+    int64_t pool_entries, subqueue_entries;
+    int64_t graph_replay;   /* 1 when the steps ran as hipGraph replays       */
 } pastar_result;
 
 typedef struct pastar_ctx pastar_ctx;

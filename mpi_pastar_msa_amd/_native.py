@@ -44,11 +44,14 @@ class pastar_search_opts(ctypes.Structure):
     _fields_ = [
         ("batch_nodes", ctypes.c_int64),
         ("table_slots_log2", ctypes.c_int64),
-        ("near_capacity", ctypes.c_int64),
-        ("far_capacity", ctypes.c_int64),
+        ("pool_entries", ctypes.c_int64),
+        ("subqueue_entries", ctypes.c_int64),
         ("max_steps", ctypes.c_int64),
+        ("band", ctypes.c_int64),
         ("profile", ctypes.c_int32),
         ("verbose", ctypes.c_int32),
+        ("no_autogrow", ctypes.c_int32),
+        ("eager", ctypes.c_int32),
     ]
 
 
@@ -68,6 +71,11 @@ class pastar_result(ctypes.Structure):
         ("expand_ms", ctypes.c_double),
         ("expand_launches", ctypes.c_int64),
         ("expand_parents", ctypes.c_int64),
+        ("capacity_retries", ctypes.c_int64),
+        ("table_slots", ctypes.c_int64),
+        ("pool_entries", ctypes.c_int64),
+        ("subqueue_entries", ctypes.c_int64),
+        ("graph_replay", ctypes.c_int64),
     ]
 
     def as_dict(self):

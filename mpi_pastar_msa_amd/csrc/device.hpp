@@ -11,7 +11,8 @@
 //                  word 0..KW-1  packed coordinate (bit 63 set = written)
 //                  word KW       best = g << 32 | parent mask  (atomicMin)
 //                  word KW+1     lo: closed_g (atomicMin), hi: h
-//   near / far   open piles of 8-B entries {slot, f}
+//   queues       open list: f-bucketed FIFO queues of 8-B entries {slot, f}
+//                (kernels.hpp "Search kernels")
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,7 +23,6 @@ namespace dev {
 
 constexpr int kMaxN = 16;
 constexpr int kMaxPairs = kMaxN * (kMaxN - 1) / 2;
-constexpr int kHistBins = 1024;       // f histogram of the near pile
 constexpr int kBlock = 256;           // threads per block (4 waves)
 constexpr int kWaves = kBlock / 64;
 constexpr int kTPerWave = 512;        // int2 pair-corner terms per wave (LDS)
@@ -54,26 +54,19 @@ struct Entry {  // open-pile entry
 
 // Per-step counters (two sets, alternating with the step parity).
 struct StepStats {
-    unsigned long long near_count;    // entries in the next near pile
-    unsigned long long far_count;     // entries appended to the far pile
-    unsigned long long batch_count;   // entries selected for expansion
+    unsigned long long pad0[3];
     unsigned long long expanded;      // parents that passed stale/closed checks
     unsigned long long reopen;
     unsigned long long generated;     // border-valid children
     unsigned long long claimed;       // new table slots
     unsigned long long outbox_total;
-    unsigned long long overflow;      // capacity or probe-limit failures
+    unsigned long long ovf_near;      // chunk pool exhausted
+    unsigned long long ovf_far;       // sub-queue chunk table exhausted
+    unsigned long long ovf_table;     // node table probe limit hit
+    unsigned long long ovf_out;       // outbox capacity exceeded
     unsigned long long dropped;       // pruned by f >= bound / stale
-    unsigned long long pad[6];
+    unsigned long long pad[3];
     unsigned long long outbox_count[8];
-    unsigned int hist[kHistBins];
-};
-
-struct FarStats {
-    int min_f;
-    int pad;
-    unsigned long long live;
-    unsigned int hist[kHistBins];
 };
 
 // Remote record sent to the owner shard over RCCL.

@@ -196,24 +196,72 @@ __global__ __launch_bounds__(kBlock) void expand_api_kernel(const DevProblem *__
 }
 
 // ---------------------------------------------------------------------------
-// Search kernels
+// Search kernels.
+//
+// Open list: f-bucketed FIFO queues.  Bucket b holds the open entries with
+// f in [f0 + b*band, f0 + (b+1)*band) (the last bucket also everything
+// above).  Each bucket is split into kSub sub-queues (a block appends to
+// sub-queue blockIdx % kSub, so an append counter is shared by one XCD's
+// blocks only), and a sub-queue is a list of kChunk-entry chunks taken from a
+// pool by a bump allocator.  Positions are 64-bit counters: W (reserved by
+// appends) and R (consumed by batches).  Nothing is ever rewritten.
+//
+// One step is two launches that read their plan from the device-resident
+// Ctl block, so runs of steps are replayed as one hipGraph:
+//   select  (1 block): book-keeping, find the lowest bucket with entries,
+//                      cut a batch of at most kmax entries from it
+//   expand           : expand the batch, relax children, append improved ones
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void hist_add(unsigned int *h, int f, int base)
+constexpr int kSub = 32;           // sub-queues per bucket
+constexpr int kBuckets = 2048;     // f buckets
+constexpr int kChunkLog2 = 12;     // entries per chunk = 4096 (32 KB)
+constexpr int kChunk = 1 << kChunkLog2;
+constexpr uint32_t kNoChunk = 0xffffffffu;
+
+enum { kFailNear = 1, kFailFar = 2, kFailTable = 4, kFailOut = 8 };  // near = chunk pool, far = chunk table
+
+__host__ __device__ inline int fail_bits(const StepStats &s)
 {
-    int b = f - base;
-    b = b < 0 ? 0 : (b > kHistBins - 1 ? kHistBins - 1 : b);
-    atomicAdd(&h[b], 1u);
+    return (s.ovf_near ? kFailNear : 0) | (s.ovf_far ? kFailFar : 0) | (s.ovf_table ? kFailTable : 0) |
+           (s.ovf_out ? kFailOut : 0);
 }
 
-__device__ __forceinline__ void hist_flush(unsigned int *lds_hist, unsigned int *global_hist)
-{
-    __syncthreads();
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
-        const unsigned int v = lds_hist[b];
-        if (v)
-            atomicAdd(&global_hist[b], v);
-    }
-}
+struct Ctl {
+    int status;     // 0 running, 1 done, 2 capacity exhausted, 3 step limit
+    int band_log2;  // bucket width = 2^band_log2
+    int f0;         // f of bucket 0 (h of the origin)
+    int cur_b;      // lowest bucket that may hold entries (f_min only grows)
+    int batch_b;    // bucket of the current batch
+    int n_shards;
+    int fail_mask;  // kFail* bits of the capacity that ran out
+    int has_work;   // select found a live bucket (multi-shard termination)
+    unsigned long long kmax;
+    unsigned long long pool_top, pool_chunks, maxch;
+    unsigned long long table_slots;
+    unsigned long long n_batch;
+    unsigned long long b_start[kSub], b_cnt[kSub], b_prefix[kSub + 1];
+    long long steps, max_steps;
+    unsigned long long expanded, reopen, generated, claimed, dropped, parents;
+};
+
+struct Queues {
+    unsigned long long W[kBuckets][kSub];
+    unsigned long long R[kBuckets][kSub];
+};
+
+struct SearchArgs {
+    const DevProblem *P;
+    Ctl *ctl;
+    uint64_t *table;
+    uint64_t cap_mask;
+    Queues *q;
+    uint32_t *chunk_tab;  // [kBuckets][kSub][maxch], chunk id + 1
+    Entry *pool;          // [pool_chunks][kChunk]
+    StepStats *stats;
+    int *goal_g;
+    void *outbox;  // Remote<KW>[n_shards][outbox_cap]
+    unsigned long long outbox_cap;
+};
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
@@ -223,87 +271,69 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
-// Split the near pile: f <= t -> batch (at most kmax), t < f < bound -> the
-// next near pile (with its f histogram relative to `base`), f >= bound -> drop.
-// Block 0 also clears the other parity's StepStats for the next step.
-__global__ __launch_bounds__(kBlock) void partition_kernel(const Entry *__restrict__ in, unsigned long long n,
-                                                           int t, int bound, int base,
-                                                           unsigned long long kmax, Entry *__restrict__ batch,
-                                                           Entry *__restrict__ keep, unsigned long long keep_cap,
-                                                           StepStats *__restrict__ st, StepStats *__restrict__ st_next)
+__device__ __forceinline__ int bucket_of(int f, int f0, int w)
 {
-    __shared__ unsigned int lh[kHistBins];
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
-        lh[b] = 0;
-    if (blockIdx.x == 0) {
-        unsigned long long *z = (unsigned long long *)st_next;
-        const int words = (int)(sizeof(StepStats) / 8);
-        for (int w = threadIdx.x; w < words; w += blockDim.x)
-            z[w] = 0;
-    }
-    __syncthreads();
-    unsigned long long dropped = 0;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    const unsigned long long start = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long iters = (n + stride - 1) / stride;
-    const int lane = lane_id();
-    for (unsigned long long it = 0; it < iters; it++) {
-        const unsigned long long i = start + it * stride;
-        Entry e = {0, 0};
-        const bool in_range = i < n;
-        if (in_range)
-            e = in[i];
-        const bool drop = in_range && e.f >= bound;
-        const bool sel = in_range && !drop && e.f <= t;
-        dropped += drop;
-        const uint64_t mask = __ballot(sel);
-        unsigned long long bbase = 0;
-        if (mask) {
-            const int leader = __ffsll((long long)mask) - 1;
-            if (lane == leader)
-                bbase = atomicAdd(&st->batch_count, (unsigned long long)__popcll(mask));
-            bbase = __shfl(bbase, leader);
-        }
-        const unsigned long long idx = bbase + __popcll(mask & ((1ull << lane) - 1ull));
-        const bool to_batch = sel && idx < kmax;
-        if (to_batch)
-            batch[idx] = e;
-        const bool to_keep = in_range && !drop && !to_batch;
-        if (to_keep)
-            hist_add(lh, e.f, base);
-        wave_append(to_keep, &st->near_count, keep, keep_cap, e, &st->overflow);
-    }
-    dropped = wave_sum(dropped);
-    if (lane == 0 && dropped)
-        atomicAdd(&st->dropped, dropped);
-    hist_flush(lh, st->hist);
+    const long long b = ((long long)f - f0) >> w;
+    return b < 0 ? 0 : (b >= kBuckets ? kBuckets - 1 : (int)b);
 }
 
-struct SearchArgs {
-    const DevProblem *P;
-    uint64_t *table;
-    uint64_t cap_mask;
-    const Entry *batch;
-    unsigned long long kmax;
-    StepStats *st;
-    Entry *near_out;
-    unsigned long long near_cap;
-    Entry *far_out;
-    unsigned long long *far_n;
-    unsigned long long far_cap;
-    void *outbox;  // Remote<KW>[n_shards][outbox_cap]
-    unsigned long long outbox_cap;
-    int *goal_g;
-    int t_near, bound, base, pad;
-};
+// Write entry e at position p of sub-queue (b, sq).  The lane whose position
+// opens a chunk allocates it; the others wait for its publication (the
+// allocating wave reserved an earlier range, so it is resident and past its
+// reservation).
+__device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, unsigned long long p, const Entry &e,
+                                            StepStats *st)
+{
+    const unsigned long long k = p >> kChunkLog2;
+    const unsigned off = (unsigned)(p & (kChunk - 1));
+    const unsigned long long maxch = a.ctl->maxch;
+    if (k >= maxch) {
+        atomicAdd(&st->ovf_far, 1ull);
+        return;
+    }
+    uint32_t *tp = a.chunk_tab + ((size_t)b * kSub + sq) * maxch + k;
+    if (off == 0) {
+        const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
+        const uint32_t v = id < a.ctl->pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
+        __hip_atomic_store(tp, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint32_t c;
+    while ((c = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    if (c == kNoChunk) {
+        atomicAdd(&st->ovf_near, 1ull);
+        return;
+    }
+    a.pool[(size_t)(c - 1) * kChunk + off] = e;
+}
 
-// Route one child: relax locally or post it to its owner shard; append the
-// improved ones to the near / far pile.  All lanes of the wave must call it.
+// Wave-aggregated append of the predicated lanes' entries to their buckets:
+// one atomic per distinct bucket in the wave.  Every lane must call it.
+__device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int b, const Entry &e, StepStats *st)
+{
+    const int sq = blockIdx.x % kSub;
+    const int lane = lane_id();
+    uint64_t pending = __ballot(pred);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int bl = __shfl(b, leader);
+        const uint64_t m = __ballot(pred && b == bl) & pending;
+        unsigned long long base = 0;
+        if (lane == leader)
+            base = atomicAdd(&a.q->W[bl][sq], (unsigned long long)__popcll(m));
+        base = __shfl(base, leader);
+        if ((m >> lane) & 1ull)
+            queue_store(a, bl, sq, base + __popcll(m & ((1ull << lane) - 1ull)), e, st);
+        pending &= ~m;
+    }
+}
+
+// Route one child: relax locally or post it to its owner shard; queue the
+// improved ones.  All lanes of the wave must call it.
 template <int KW>
-__device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, bool valid, bool local,
-                                            int owner, const uint64_t (&ck)[KW], int g, int h, int m,
-                                            unsigned int *lh, unsigned long long &claimed,
-                                            unsigned long long &ovf)
+__device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
+                                            bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
+                                            int m, unsigned long long &claimed, unsigned long long &ovf)
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
@@ -317,44 +347,140 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
         if (improved) {
             bool goal = true;
 #pragma unroll
-            for (int w = 0; w < KW; w++)
-                goal &= (ck[w] == P.goal_key[w]);
+            for (int k = 0; k < KW; k++)
+                goal &= (ck[k] == P.goal_key[k]);
             if (goal)
                 atomicMin(a.goal_g, g);
         }
     }
     const int f = g + h;
     const Entry e = {(uint32_t)slot, f};
-    const bool near = improved && f < a.t_near;
-    const bool far = improved && f >= a.t_near;
-    if (near)
-        hist_add(lh, f, a.base);
-    wave_append(near, &a.st->near_count, a.near_out, a.near_cap, e, &a.st->overflow);
-    wave_append(far, a.far_n, a.far_out, a.far_cap, e, &a.st->overflow);
+    queue_append(a, improved, bucket_of(f, f0, w), e, st);
     if (P.n_shards > 1) {
         const bool remote = valid && !local;
         Remote<KW> rec;
 #pragma unroll
-        for (int w = 0; w < KW; w++)
-            rec.key[w] = ck[w];
+        for (int k = 0; k < KW; k++)
+            rec.key[k] = ck[k];
         rec.g = g;
         rec.h = h;
         rec.pmask = m;
         rec.pad = 0;
         Remote<KW> *ob = (Remote<KW> *)a.outbox;
         for (int d = 0; d < P.n_shards; d++)
-            wave_append(remote && owner == d, &a.st->outbox_count[d], ob + (size_t)d * a.outbox_cap,
-                        a.outbox_cap, rec, &a.st->overflow);
+            wave_append(remote && owner == d, &st->outbox_count[d], ob + (size_t)d * a.outbox_cap, a.outbox_cap,
+                        rec, &st->ovf_out);
     }
 }
 
-// One search step: expand every entry of the batch (worker_inner's dequeue,
-// closed check and getNeigh, PAStar.cpp:320-401) and relax its neighbours
-// into the node table (PAStar::enqueue + conditional_enqueue, :219-237).
+// select: account the previous step, then cut the next batch from the lowest
+// bucket holding entries below the best goal (PAStar::check_stop's
+// termination, PAStar.cpp:480-547: the goal is accepted once no open node has
+// f below its g).  One block of kBlock threads.
+__global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
+{
+    Ctl *ctl = a.ctl;
+    if (ctl->status)
+        return;
+    StepStats *st = a.stats;
+    const int tid = threadIdx.x;
+    __shared__ int found;
+    __shared__ unsigned long long avail[kSub];
+    if (tid == 0) {
+        ctl->expanded += st->expanded;
+        ctl->reopen += st->reopen;
+        ctl->generated += st->generated;
+        ctl->claimed += st->claimed;
+        ctl->dropped += st->dropped;
+        ctl->parents += ctl->n_batch;
+        int fm = fail_bits(*st);
+        if (ctl->claimed * 10 > ctl->table_slots * 7)
+            fm |= kFailTable;
+        if (fm) {
+            ctl->fail_mask |= fm;
+            ctl->status = 2;
+        }
+        found = kBuckets;
+    }
+    __syncthreads();
+    if (ctl->status)
+        return;
+    unsigned long long *z = (unsigned long long *)st;
+    for (int k = tid; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
+        z[k] = 0;
+    const int goal = *(volatile int *)a.goal_g;
+    const int w = ctl->band_log2, f0 = ctl->f0;
+    const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
+    constexpr int per = kBlock / kSub;  // buckets examined per round
+    for (int b0 = ctl->cur_b; b0 <= limit; b0 += per) {
+        const int b = b0 + tid / kSub, sq = tid % kSub;
+        if (b <= limit && a.q->W[b][sq] > a.q->R[b][sq])
+            atomicMin(&found, b);
+        __syncthreads();
+        if (found < kBuckets)
+            break;
+    }
+    const int b = found;
+    if (b >= kBuckets) {
+        if (tid == 0) {
+            ctl->n_batch = 0;
+            ctl->has_work = 0;
+            ctl->cur_b = limit + 1 < kBuckets ? limit + 1 : kBuckets - 1;
+            if (ctl->n_shards == 1)
+                ctl->status = 1;
+            ctl->steps++;
+            if (ctl->max_steps && ctl->steps >= ctl->max_steps && !ctl->status)
+                ctl->status = 3;
+        }
+        return;
+    }
+    if (tid < kSub)
+        avail[tid] = a.q->W[b][tid] - a.q->R[b][tid];
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long left = ctl->kmax, pre = 0;
+        for (int sq = 0; sq < kSub; sq++) {
+            const unsigned long long take = avail[sq] < left ? avail[sq] : left;
+            ctl->b_start[sq] = a.q->R[b][sq];
+            ctl->b_cnt[sq] = take;
+            ctl->b_prefix[sq] = pre;
+            a.q->R[b][sq] += take;
+            pre += take;
+            left -= take;
+        }
+        ctl->b_prefix[kSub] = pre;
+        ctl->n_batch = pre;
+        ctl->batch_b = b;
+        ctl->cur_b = b;
+        ctl->has_work = 1;
+        ctl->steps++;
+        if (ctl->max_steps && ctl->steps >= ctl->max_steps)
+            ctl->status = 3;
+    }
+}
+
+// Entry i of the current batch.
+__device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl, const unsigned long long *prefix,
+                                             unsigned long long i)
+{
+    int sq = 0;
+    while (sq + 1 < kSub && prefix[sq + 1] <= i)
+        sq++;
+    const unsigned long long p = ctl->b_start[sq] + (i - prefix[sq]);
+    const uint32_t c = a.chunk_tab[((size_t)ctl->batch_b * kSub + sq) * ctl->maxch + (p >> kChunkLog2)];
+    return a.pool[(size_t)(c - 1) * kChunk + (p & (kChunk - 1))];
+}
+
+// expand every entry of the batch (worker_inner's dequeue, closed check and
+// getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
+// (PAStar::enqueue + conditional_enqueue, :219-237).
 template <int N, int KW>
 __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
+    Ctl *ctl = a.ctl;
+    if (ctl->status)
+        return;
     const DevProblem &P = *a.P;
     const int n = N ? N : P.n;
     const int npairs = P.npairs;
@@ -364,13 +490,14 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
     __shared__ int2 terms_all[kWaves][kTPerWave];
-    __shared__ unsigned int lh[kHistBins];
+    __shared__ unsigned long long prefix[kSub + 1];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
-        lh[b] = 0;
-    const unsigned long long nb = a.st->batch_count < a.kmax ? a.st->batch_count : a.kmax;
-    int bound = *(volatile int *)a.goal_g;
-    bound = bound < a.bound ? bound : a.bound;
+    if (threadIdx.x <= kSub)
+        prefix[threadIdx.x] = ctl->b_prefix[threadIdx.x];
+    StepStats *st = a.stats;
+    const int w = ctl->band_log2, f0 = ctl->f0;
+    const unsigned long long nb = ctl->n_batch;
+    const int bound = *(volatile int *)a.goal_g;
     unsigned long long expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
     const int per_block = kWaves * npw;
     const int masks = 1 << n;
@@ -378,28 +505,28 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
         const unsigned long long node = chunk * per_block + wave * npw + group;
         bool ok = node < nb;
-        Parent<N, KW> par;
-        par.g = 0;
-        par.pmask = 0;
-        par.blocked = 0;
+        Parent<N, KW> par_;
+        par_.g = 0;
+        par_.pmask = 0;
+        par_.blocked = 0;
 #pragma unroll
-        for (int w = 0; w < KW; w++)
-            par.key[w] = 0;
+        for (int k = 0; k < KW; k++)
+            par_.key[k] = 0;
         if (ok) {
-            const Entry e = a.batch[node];
+            const Entry e = batch_entry(a, ctl, prefix, node);
             const uint64_t *s = a.table + (uint64_t)e.slot * SW;
 #pragma unroll
-            for (int w = 0; w < KW; w++)
-                par.key[w] = s[w];
+            for (int k = 0; k < KW; k++)
+                par_.key[k] = s[k];
             const uint64_t best = s[KW];
             const int h = (int)(s[KW + 1] >> 32);
-            par.g = (int)(best >> 32);
-            par.pmask = (int)(uint32_t)best;
-            ok = (par.g + h == e.f) && e.f < bound;
+            par_.g = (int)(best >> 32);
+            par_.pmask = (int)(uint32_t)best;
+            ok = (par_.g + h == e.f) && e.f < bound;
             int verdict = ok ? 1 : 0;
             if (ok && glane == 0) {
-                const int old = atomicMin((int *)(a.table + (uint64_t)e.slot * SW + KW + 1), par.g);
-                verdict = old <= par.g ? 0 : (old != kIntMax ? 2 : 1);
+                const int old = atomicMin((int *)(a.table + (uint64_t)e.slot * SW + KW + 1), par_.g);
+                verdict = old <= par_.g ? 0 : (old != kIntMax ? 2 : 1);
             }
             verdict = __shfl(verdict, leader_lane);
             ok = verdict != 0;
@@ -410,45 +537,44 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             }
         }
         if (ok) {
-            decode_key<N, KW>(P, n, par.key, par.pos);
+            decode_key<N, KW>(P, n, par_.key, par_.pos);
 #pragma unroll
             for (int i = 0; i < Parent<N, KW>::NMAX; i++)
-                if ((N || i < n) && par.pos[i] >= P.len[i])
-                    par.blocked |= 1 << i;
-            stage_terms<N, KW>(P, n, npairs, par, terms, glane, lpn);
+                if ((N || i < n) && par_.pos[i] >= P.len[i])
+                    par_.blocked |= 1 << i;
+            stage_terms<N, KW>(P, n, npairs, par_, terms, glane, lpn);
         }
         __syncthreads();
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
-            bool valid = ok && m >= 1 && m < masks && !(m & par.blocked);
+            bool valid = ok && m >= 1 && m < masks && !(m & par_.blocked);
             int g = 0, h = 0, owner = P.shard;
             uint64_t ck[KW];
 #pragma unroll
-            for (int w = 0; w < KW; w++)
-                ck[w] = 0;
+            for (int k = 0; k < KW; k++)
+                ck[k] = 0;
             if (valid) {
                 const int2 dc = child_cost<N>(P, npairs, terms, m);
-                g = par.g + dc.x;
+                g = par_.g + dc.x;
                 h = dc.y;
                 generated++;
                 if (g + h >= bound)
                     valid = false;
             }
             if (valid) {
-                child_key<N, KW>(P, n, par.key, m, ck);
+                child_key<N, KW>(P, n, par_.key, m, ck);
                 if (P.n_shards > 1) {
                     int cp[Parent<N, KW>::NMAX];
 #pragma unroll
                     for (int i = 0; i < Parent<N, KW>::NMAX; i++)
-                        cp[i] = par.pos[i] + ((m >> i) & 1);
+                        cp[i] = par_.pos[i] + ((m >> i) & 1);
                     owner = owner_dev<Parent<N, KW>::NMAX>(P, n, cp, P.n_shards);
                 }
             }
-            route_child<KW>(a, P, valid, owner == P.shard, owner, ck, g, h, m, lh, claimed, ovf);
+            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf);
         }
         __syncthreads();
     }
-    hist_flush(lh, a.st->hist);
     expanded = wave_sum(expanded);
     reopen = wave_sum(reopen);
     generated = wave_sum(generated);
@@ -457,17 +583,17 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     stale = wave_sum(stale);
     if (lane == 0) {
         if (expanded)
-            atomicAdd(&a.st->expanded, expanded);
+            atomicAdd(&st->expanded, expanded);
         if (reopen)
-            atomicAdd(&a.st->reopen, reopen);
+            atomicAdd(&st->reopen, reopen);
         if (generated)
-            atomicAdd(&a.st->generated, generated);
+            atomicAdd(&st->generated, generated);
         if (claimed)
-            atomicAdd(&a.st->claimed, claimed);
+            atomicAdd(&st->claimed, claimed);
         if (ovf)
-            atomicAdd(&a.st->overflow, ovf);
+            atomicAdd(&st->ovf_table, ovf);
         if (stale)
-            atomicAdd(&a.st->dropped, stale);
+            atomicAdd(&st->dropped, stale);
     }
 }
 
@@ -478,12 +604,10 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
                                                                unsigned long long count)
 {
     const DevProblem &P = *a.P;
-    __shared__ unsigned int lh[kHistBins];
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
-        lh[b] = 0;
-    __syncthreads();
-    int bound = *(volatile int *)a.goal_g;
-    bound = bound < a.bound ? bound : a.bound;
+    Ctl *ctl = a.ctl;
+    StepStats *st = a.stats;
+    const int w = ctl->band_log2, f0 = ctl->f0;
+    const int bound = *(volatile int *)a.goal_g;
     unsigned long long claimed = 0, ovf = 0;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     const unsigned long long iters = (count + stride - 1) / stride;
@@ -493,106 +617,39 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
         uint64_t ck[KW];
         int g = 0, h = 0, m = 0;
 #pragma unroll
-        for (int w = 0; w < KW; w++)
-            ck[w] = 0;
+        for (int k = 0; k < KW; k++)
+            ck[k] = 0;
         if (valid) {
             const Remote<KW> r = recs[i];
 #pragma unroll
-            for (int w = 0; w < KW; w++)
-                ck[w] = r.key[w];
+            for (int k = 0; k < KW; k++)
+                ck[k] = r.key[k];
             g = r.g;
             h = r.h;
             m = r.pmask;
             valid = g + h < bound;
         }
-        route_child<KW>(a, P, valid, true, P.shard, ck, g, h, m, lh, claimed, ovf);
+        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf);
     }
-    hist_flush(lh, a.st->hist);
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);
     if (lane_id() == 0) {
         if (claimed)
-            atomicAdd(&a.st->claimed, claimed);
+            atomicAdd(&st->claimed, claimed);
         if (ovf)
-            atomicAdd(&a.st->overflow, ovf);
+            atomicAdd(&st->ovf_table, ovf);
     }
 }
 
-// Far pile statistics: min f and live count over f < bound.
-__global__ __launch_bounds__(kBlock) void far_min_kernel(const Entry *__restrict__ far, unsigned long long n,
-                                                         int bound, FarStats *__restrict__ fs)
+// Open entries left in the queues (live or stale), for the statistics.
+__global__ void queue_census_kernel(const Queues *__restrict__ q, unsigned long long *__restrict__ out)
 {
-    int mn = kIntMax;
-    unsigned long long live = 0;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int f = far[i].f;
-        if (f < bound) {
-            mn = f < mn ? f : mn;
-            live++;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int v = __shfl_xor(mn, o);
-        mn = v < mn ? v : mn;
-    }
-    live = wave_sum(live);
-    if (lane_id() == 0) {
-        if (mn != kIntMax)
-            atomicMin(&fs->min_f, mn);
-        if (live)
-            atomicAdd(&fs->live, live);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void far_hist_kernel(const Entry *__restrict__ far, unsigned long long n,
-                                                          int bound, int base, FarStats *__restrict__ fs)
-{
-    __shared__ unsigned int lh[kHistBins];
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
-        lh[b] = 0;
-    __syncthreads();
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int f = far[i].f;
-        if (f < bound)
-            hist_add(lh, f, base);
-    }
-    hist_flush(lh, fs->hist);
-}
-
-// Move far entries with f < t_near into the near pile (appended after
-// `near_off` existing entries, histogram relative to `base`); keep
-// t_near <= f < bound in the other far buffer; drop f >= bound.
-__global__ __launch_bounds__(kBlock) void far_partition_kernel(const Entry *__restrict__ in, unsigned long long n,
-                                                               int t_near, int bound, int base,
-                                                               Entry *__restrict__ near_out,
-                                                               unsigned long long near_cap,
-                                                               Entry *__restrict__ far_out,
-                                                               unsigned long long far_cap, StepStats *__restrict__ st)
-{
-    __shared__ unsigned int lh[kHistBins];
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
-        lh[b] = 0;
-    __syncthreads();
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    const unsigned long long iters = (n + stride - 1) / stride;
-    for (unsigned long long it = 0; it < iters; it++) {
-        const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x + it * stride;
-        Entry e = {0, 0};
-        const bool in_range = i < n;
-        if (in_range)
-            e = in[i];
-        const bool live = in_range && e.f < bound;
-        const bool to_near = live && e.f < t_near;
-        const bool to_far = live && e.f >= t_near;
-        if (to_near)
-            hist_add(lh, e.f, base);
-        wave_append(to_near, &st->near_count, near_out, near_cap, e, &st->overflow);
-        wave_append(to_far, &st->far_count, far_out, far_cap, e, &st->overflow);
-    }
-    hist_flush(lh, st->hist);
+    unsigned long long s = 0;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < kBuckets * kSub; k += gridDim.x * blockDim.x)
+        s += q->W[k / kSub][k % kSub] - q->R[k / kSub][k % kSub];
+    s = wave_sum(s);
+    if (lane_id() == 0 && s)
+        atomicAdd(out, s);
 }
 
 // Backtrace walk (backtrace.cpp:47-69): from `start`, follow parent masks,

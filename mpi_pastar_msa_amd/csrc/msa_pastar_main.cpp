@@ -7,7 +7,7 @@
 // backtrace.cpp:20-191, PAStar.cpp:591-619).  MPI ranks become GPU shards:
 //   --gpus G   one process per GPU (forked before any HIP call), nodes routed
 //              by the same z-order owner hash, exchanged over RCCL.
-// Engine knobs: --batch K, --table-log2 L, --far-capacity F, --verbose.
+// Engine knobs: --batch K, --table-log2 L, --pool E, --verbose.
 #include <sys/ioctl.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -31,7 +31,7 @@ struct Options {
     int hash_shift = 12;
     int hash_type = PASTAR_HASH_FZORDER;
     int gpus = 1;
-    long long batch = 0, table_log2 = 0, far_capacity = 0;
+    long long batch = 0, table_log2 = 0, pool = 0;
     bool verbose = false;
     std::string file;
 };
@@ -52,7 +52,7 @@ void usage(const char *argv0)
               << "  --gpus arg (=1)           GPU shards (one process per GPU)\n"
               << "  --batch arg               open nodes expanded per step\n"
               << "  --table-log2 arg          node table capacity (log2 slots)\n"
-              << "  --far-capacity arg        far open pile capacity (entries)\n"
+              << "  --pool arg                open-list entry pool (entries)\n"
               << std::endl;
 }
 
@@ -113,10 +113,10 @@ int parse(int argc, char **argv, Options &o)
             if (!(v = need(i)))
                 return -1;
             o.table_log2 = std::atoll(v);
-        } else if (a == "--far-capacity") {
+        } else if (a == "--pool") {
             if (!(v = need(i)))
                 return -1;
-            o.far_capacity = std::atoll(v);
+            o.pool = std::atoll(v);
         } else if (!a.empty() && a[0] == '-') {
             std::cerr << "Invalid argument: unrecognised option '" << a << "'\n";
             return -1;
@@ -225,7 +225,7 @@ int run_shard(const Options &o, int rank, const unsigned char *rid, ShardReport 
     pastar_search_opts so{};
     so.batch_nodes = o.batch;
     so.table_slots_log2 = o.table_log2;
-    so.far_capacity = o.far_capacity;
+    so.pool_entries = o.pool;
     so.verbose = o.verbose;
     t = now();
     CHECK(pastar_gpu_search(ctx, &so, &report->r));

@@ -125,20 +125,26 @@ struct pastar_ctx {
     // search state
     DevBuf<uint64_t> table;
     uint64_t nslots = 0;
-    DevBuf<Entry> near_buf[2], far_buf[2], batch;
-    DevBuf<StepStats> stats;  // [0], [1] step parity, [2] refill
-    DevBuf<FarStats> farstats;
-    DevBuf<unsigned long long> far_n;
+    DevBuf<Queues> queues;
+    DevBuf<uint32_t> chunk_tab;
+    DevBuf<Entry> pool;
+    DevBuf<StepStats> stats;
+    DevBuf<Ctl> ctl;
     DevBuf<int> goal;
     DevBuf<uint8_t> outbox, inbox;
     DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
     StepStats *h_stats = nullptr;         // pinned
-    FarStats *h_far = nullptr;            // pinned
+    Ctl *h_ctl = nullptr;                 // pinned
     bool searched = false;
     int64_t score = -1;
     // capacities of the current search buffers (reused across searches)
-    unsigned long long cap_kmax = 0, cap_near = 0, cap_far = 0, cap_outbox = 0;
+    unsigned long long cap_kmax = 0, cap_pool = 0, cap_maxch = 0, cap_outbox = 0;
     int cap_log2 = 0;
+    // capacities learned by automatic growth, kept for later searches
+    unsigned long long grown_pool = 0, grown_maxch = 0, grown_outbox = 0;
+    int grown_log2 = 0;
+    int last_fail_mask = 0;
+    bool graph_used = false;
 };
 
 namespace {
@@ -449,7 +455,7 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
         NCCL_TRY(ncclCommInitRank(&c->comm, n_shards, id, shard_rank));
     }
     HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&c->h_far, sizeof(FarStats), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
     *out = c.release();
     return PASTAR_OK;
 }
@@ -465,8 +471,8 @@ void pastar_gpu_destroy(pastar_ctx *c)
         ncclCommDestroy(c->comm);
     if (c->h_stats)
         (void)hipHostFree(c->h_stats);
-    if (c->h_far)
-        (void)hipHostFree(c->h_far);
+    if (c->h_ctl)
+        (void)hipHostFree(c->h_ctl);
     if (c->ev0)
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
@@ -602,29 +608,33 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
 namespace {
 
 struct SearchCfg {
-    unsigned long long kmax, near_cap, far_cap, outbox_cap;
+    unsigned long long kmax, pool_entries, subqueue_entries, outbox_cap;
     int table_log2;
-    int verbose, profile;
+    int verbose, profile, eager;
     int64_t max_steps;
+    int64_t band;
 };
+
+unsigned long long maxch_of(const SearchCfg &cfg) { return (cfg.subqueue_entries + kChunk - 1) / kChunk; }
+unsigned long long pool_chunks_of(const SearchCfg &cfg) { return (cfg.pool_entries + kChunk - 1) / kChunk; }
 
 int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
 {
     const int sw = slot_words_rt(c->kw);
+    const unsigned long long maxch = maxch_of(cfg), chunks = pool_chunks_of(cfg);
     const bool same = c->table.p && c->cap_log2 == cfg.table_log2 && c->cap_kmax == cfg.kmax &&
-                      c->cap_near == cfg.near_cap && c->cap_far == cfg.far_cap && c->cap_outbox == cfg.outbox_cap;
+                      c->cap_pool == chunks && c->cap_maxch == maxch && c->cap_outbox == cfg.outbox_cap;
     if (!same) {
         c->table.reset();  // free before allocating the next set
+        c->pool.reset();
+        c->chunk_tab.reset();
         c->nslots = 1ull << cfg.table_log2;
         PA_TRY(c->table.alloc((size_t)c->nslots * sw));
-        PA_TRY(c->near_buf[0].alloc(cfg.near_cap));
-        PA_TRY(c->near_buf[1].alloc(cfg.near_cap));
-        PA_TRY(c->far_buf[0].alloc(cfg.far_cap));
-        PA_TRY(c->far_buf[1].alloc(cfg.far_cap));
-        PA_TRY(c->batch.alloc(cfg.kmax));
-        PA_TRY(c->stats.alloc(3));
-        PA_TRY(c->farstats.alloc(1));
-        PA_TRY(c->far_n.alloc(1));
+        PA_TRY(c->queues.alloc(1));
+        PA_TRY(c->chunk_tab.alloc((size_t)kBuckets * kSub * maxch));
+        PA_TRY(c->pool.alloc((size_t)chunks * kChunk));
+        PA_TRY(c->stats.alloc(1));
+        PA_TRY(c->ctl.alloc(1));
         PA_TRY(c->goal.alloc(1));
         if (c->n_shards > 1) {
             const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
@@ -634,8 +644,8 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         }
         c->cap_log2 = cfg.table_log2;
         c->cap_kmax = cfg.kmax;
-        c->cap_near = cfg.near_cap;
-        c->cap_far = cfg.far_cap;
+        c->cap_pool = chunks;
+        c->cap_maxch = maxch;
         c->cap_outbox = cfg.outbox_cap;
     }
     const int blocks = (int)std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock);
@@ -644,31 +654,11 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     else
         hipLaunchKernelGGL((init_table_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
     PA_TRY(check_launch());
-    HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats) * 3, c->stream));
-    HIP_TRY(hipMemsetAsync(c->far_n.p, 0, sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
+    HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
+    HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
     return PASTAR_OK;
-}
-
-// choose the batch threshold: smallest f with at least `target` entries <= f
-int pick_threshold(const unsigned int *hist, int base, unsigned long long target, unsigned long long *selected,
-                   int *fmin)
-{
-    unsigned long long cum = 0;
-    int first = -1;
-    for (int b = 0; b < kHistBins; b++) {
-        if (hist[b] && first < 0)
-            first = b;
-        cum += hist[b];
-        if (cum >= target && first >= 0) {
-            *selected = cum;
-            *fmin = base + first;
-            return base + b;
-        }
-    }
-    *selected = cum;
-    *fmin = first < 0 ? kIntMax : base + first;
-    return base + kHistBins - 1;
 }
 
 int allreduce_i64(pastar_ctx *c, int64_t *vals, int count, ncclRedOp_t op)
@@ -679,6 +669,35 @@ int allreduce_i64(pastar_ctx *c, int64_t *vals, int count, ncclRedOp_t op)
     NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, op, c->comm, c->stream));
     HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
+// Bucket width (the band of f one step expands).  Default: about a third of
+// the mean f increase of one expansion of the origin, rounded to a power of
+// two, so that a node is rarely expanded before a cheaper path to it has been
+// settled (work inflation stays near the serial count) while a step still
+// holds a whole f-layer of the frontier (tools/tune.py sweeps it).
+int estimate_band_log2(pastar_ctx *c, int h0, int64_t band_opt, int *w_out)
+{
+    int64_t band = band_opt;
+    if (band <= 0) {
+        pastar_node origin{};
+        origin.g = 0;
+        origin.f = h0;
+        origin.parent_mask = (1 << c->n) - 1;
+        const int masks = (1 << c->n) - 1;
+        std::vector<pastar_node> kids((size_t)masks);
+        int64_t cnt = 0;
+        PA_TRY(pastar_gpu_expand(c, &origin, 1, 1, kids.data(), nullptr, nullptr, &cnt));
+        int64_t sum = 0;
+        for (int64_t k = 0; k < cnt; k++)
+            sum += (int64_t)kids[(size_t)k].f - h0;
+        band = cnt ? std::max<int64_t>(1, sum / cnt / 3) : 1;
+    }
+    int w = 0;
+    while ((2ll << w) <= band * 4 / 3 && w < 24)  // nearest power of two
+        w++;
+    *w_out = w;
     return PASTAR_OK;
 }
 
@@ -693,118 +712,189 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     const int per_block = kWaves * (64 / lpn);
     const size_t rb = remote_bytes(KW);
 
-    // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
-    // its owner shard
+    // h of the origin and the bucket width
     uint16_t zero[PASTAR_MAX_SEQ] = {0};
-    const int origin_owner = G > 1 ? owner_of(c->n, zero, G, c->hp.hash_type, c->hp.hash_shift) : 0;
     int32_t h0 = 0;
     {
         DevBuf<uint16_t> dpos;
         DevBuf<int32_t> dh;
         PA_TRY(dpos.alloc(PASTAR_MAX_SEQ));
         PA_TRY(dh.alloc(1));
-        HIP_TRY(hipMemcpyAsync(dpos.p, zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpy(dpos.p, zero, sizeof(zero), hipMemcpyHostToDevice));
         hipLaunchKernelGGL(h_kernel, dim3(1), dim3(64), 0, c->stream, c->dP.p, dpos.p, 1, dh.p);
         PA_TRY(check_launch());
-        HIP_TRY(hipMemcpyAsync(&h0, dh.p, 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(&h0, dh.p, 4, hipMemcpyDeviceToHost));
     }
-    int cur = 0, fcur = 0;
-    unsigned long long nn = 0, nf = 0;
-    int base = h0;  // histogram base of near[cur]
-    std::vector<unsigned int> hist(kHistBins, 0);
-    int t_near = h0 + kHistBins - 1;
-    int goal_g = kIntMax;
+    int w = 0;
+    PA_TRY(estimate_band_log2(c, h0, cfg.band, &w));
+
+    Ctl hc{};
+    hc.band_log2 = w;
+    hc.f0 = h0;
+    hc.n_shards = G;
+    hc.kmax = cfg.kmax;
+    hc.pool_chunks = pool_chunks_of(cfg);
+    hc.maxch = maxch_of(cfg);
+    hc.table_slots = c->nslots;
+    hc.max_steps = cfg.max_steps;
+    HIP_TRY(hipMemcpy(c->ctl.p, &hc, sizeof(Ctl), hipMemcpyHostToDevice));
 
     SearchArgs a{};
     a.P = c->dP.p;
+    a.ctl = c->ctl.p;
     a.table = c->table.p;
     a.cap_mask = c->nslots - 1;
-    a.batch = c->batch.p;
-    a.kmax = cfg.kmax;
-    a.near_cap = cfg.near_cap;
-    a.far_n = c->far_n.p;
-    a.far_cap = cfg.far_cap;
+    a.q = c->queues.p;
+    a.chunk_tab = c->chunk_tab.p;
+    a.pool = c->pool.p;
+    a.stats = c->stats.p;
+    a.goal_g = c->goal.p;
     a.outbox = c->outbox.p;
     a.outbox_cap = cfg.outbox_cap;
-    a.goal_g = c->goal.p;
 
-    if (c->shard == origin_owner) {
-        // relax the origin through the same insert path as remote records
+    const dim3 blk(kBlock);
+    const dim3 expand_grid((unsigned)std::min<unsigned long long>(4096, (cfg.kmax + per_block - 1) / per_block));
+
+    // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
+    // its owner shard, through the same relax path as remote records
+    const int origin_owner = G > 1 ? owner_of(c->n, zero, G, c->hp.hash_type, c->hp.hash_shift) : 0;
+    DevBuf<uint8_t> drec;
+    PA_TRY(drec.alloc(rb));
+    {
         std::vector<uint8_t> rec(rb, 0);
         uint64_t key[4];
         pack_key(c, zero, key);
         std::memcpy(rec.data(), key, 8 * KW);
         int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
         std::memcpy(rec.data() + 8 * KW, tail, 16);
-        DevBuf<uint8_t> drec;
-        PA_TRY(drec.alloc(rb));
-        HIP_TRY(hipMemcpyAsync(drec.p, rec.data(), rb, hipMemcpyHostToDevice, c->stream));
-        a.st = c->stats.p + 0;
-        a.near_out = c->near_buf[0].p;
-        a.far_out = c->far_buf[0].p;
-        a.t_near = t_near;
-        a.bound = kIntMax;
-        a.base = base;
-        ops.insert_remote(dim3(1), dim3(kBlock), c->stream, a, drec.p, 1);
-        PA_TRY(check_launch());
-        HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        nn = c->h_stats->near_count;
-        std::memcpy(hist.data(), c->h_stats->hist, sizeof(unsigned int) * kHistBins);
-        HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
+        HIP_TRY(hipMemcpy(drec.p, rec.data(), rb, hipMemcpyHostToDevice));
     }
+    if (c->shard == origin_owner) {
+        ops.insert_remote(dim3(1), blk, c->stream, a, drec.p, 1);
+        PA_TRY(check_launch());
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
 
-    int64_t expanded = 0, reopen = 0, generated = 0, claimed = 0, exchanged = 0, steps = 0;
     double expand_ms = 0;
-    int64_t launches = 0, parents = 0;
+    int64_t launches = 0, exchanged = 0;
+    Ctl h{};
     const double t0 = now_s();
-    bool done = false;
-    while (!done) {
-        if (cfg.max_steps && steps >= cfg.max_steps)
-            return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
-        const int par = (int)(steps & 1);
-        StepStats *st = c->stats.p + par;
-        StepStats *st_next = c->stats.p + (1 - par);
-        unsigned long long sel = 0;
-        int fmin = kIntMax;
-        int t = base - 1;
-        if (nn > 0)
-            t = pick_threshold(hist.data(), base, cfg.kmax, &sel, &fmin);
-        const int bound = goal_g;
-        const int new_base = nn > 0 ? fmin : base;
-        a.st = st;
-        a.near_out = c->near_buf[1 - cur].p;
-        a.far_out = c->far_buf[fcur].p;
-        a.t_near = t_near;
-        a.bound = bound;
-        a.base = new_base;
-        {
-            const unsigned long long blocks = std::min<unsigned long long>(2048, (nn + kBlock - 1) / kBlock);
-            hipLaunchKernelGGL(partition_kernel, dim3((unsigned)std::max<unsigned long long>(blocks, 1)), dim3(kBlock), 0,
-                               c->stream, c->near_buf[cur].p, nn, t, bound, new_base, cfg.kmax, c->batch.p,
-                               c->near_buf[1 - cur].p, cfg.near_cap, st, st_next);
-            PA_TRY(check_launch());
+    if (G == 1) {
+        // runs of S steps captured once, replayed until `select` reports
+        // termination (event nodes around each expand when profiling)
+        const int S = 32;
+        std::vector<hipEvent_t> evs;
+        if (cfg.profile) {
+            evs.resize(2 * S);
+            for (auto &e : evs)
+                HIP_TRY(hipEventCreate(&e));
         }
-        const unsigned long long nb = std::min<unsigned long long>(sel, cfg.kmax);
-        if (nb > 0) {
-            const unsigned long long blocks =
-                std::min<unsigned long long>(4096, (nb + per_block - 1) / per_block);
+        c->graph_used = false;
+        auto enqueue_steps = [&](bool capturing) -> hipError_t {
+            for (int k = 0; k < S; k++) {
+                hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
+                if (cfg.profile) {
+                    hipError_t e = capturing ? hipEventRecordWithFlags(evs[2 * k], c->stream, hipEventRecordExternal)
+                                             : hipEventRecord(evs[2 * k], c->stream);
+                    if (e != hipSuccess)
+                        return e;
+                }
+                ops.expand(expand_grid, blk, c->stream, a);
+                if (cfg.profile) {
+                    hipError_t e = capturing
+                                       ? hipEventRecordWithFlags(evs[2 * k + 1], c->stream, hipEventRecordExternal)
+                                       : hipEventRecord(evs[2 * k + 1], c->stream);
+                    if (e != hipSuccess)
+                        return e;
+                }
+            }
+            return hipGetLastError();
+        };
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        bool use_graph = !cfg.eager;
+        if (use_graph) {
+            hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+            hipError_t e2 = e == hipSuccess ? enqueue_steps(true) : e;
+            hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
+            if (e2 == hipSuccess && e3 == hipSuccess)
+                e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+            if (e2 != hipSuccess || e3 != hipSuccess) {
+                if (exec)
+                    (void)hipGraphExecDestroy(exec);
+                if (graph)
+                    (void)hipGraphDestroy(graph);
+                exec = nullptr;
+                graph = nullptr;
+                (void)hipGetLastError();
+                use_graph = false;
+                if (cfg.verbose)
+                    std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
+                                 hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+            }
+        }
+        long long steps_before = 0;
+        int rc = PASTAR_OK;
+        for (;;) {
+            hipError_t e = use_graph ? hipGraphLaunch(exec, c->stream) : enqueue_steps(false);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) {
+                rc = fail(PASTAR_ENODEV, "search steps failed: %s", hipGetErrorString(e));
+                break;
+            }
+            h = *c->h_ctl;
+            const long long ran = h.steps - steps_before;
+            if (cfg.profile) {
+                for (long long k = 0; k < ran && k < S; k++) {
+                    float ms = 0;
+                    if (hipEventElapsedTime(&ms, evs[2 * k], evs[2 * k + 1]) == hipSuccess)
+                        expand_ms += ms;
+                }
+            }
+            launches += ran;
+            steps_before = h.steps;
+            if (h.status)
+                break;
+            if (cfg.verbose)
+                std::fprintf(stderr, "[pastar] step %lld expanded %llu bucket %d batch %llu pool %llu chunks\n",
+                             h.steps, h.expanded, h.cur_b, h.n_batch, h.pool_top);
+        }
+        c->graph_used = use_graph;
+        if (exec)
+            (void)hipGraphExecDestroy(exec);
+        if (graph)
+            (void)hipGraphDestroy(graph);
+        for (auto &e : evs)
+            (void)hipEventDestroy(e);
+        PA_TRY(rc);
+    } else {
+        for (;;) {
+            hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
             if (cfg.profile)
                 HIP_TRY(hipEventRecord(c->ev0, c->stream));
-            ops.expand(dim3((unsigned)blocks), dim3(kBlock), c->stream, a);
-            PA_TRY(check_launch());
+            ops.expand(expand_grid, blk, c->stream, a);
             if (cfg.profile)
                 HIP_TRY(hipEventRecord(c->ev1, c->stream));
-            launches++;
-        }
-        if (G > 1) {
-            // exchange: counts, then records (grouped point-to-point over xGMI)
-            HIP_TRY(hipMemcpyAsync(c->h_stats, st, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+            PA_TRY(check_launch());
+            // exchange: counts, then the records (grouped point-to-point over xGMI)
+            HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
+            if (cfg.profile) {
+                float ms = 0;
+                HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+                expand_ms += ms;
+            }
+            launches++;
+            const int had_work = c->h_ctl->has_work;
             std::vector<unsigned long long> send(G), recv(G);
             for (int d = 0; d < G; d++)
                 send[d] = std::min<unsigned long long>(c->h_stats->outbox_count[d], cfg.outbox_cap);
+            send[c->shard] = 0;
             HIP_TRY(hipMemcpyAsync(c->xcounts.p, send.data(), 8 * G, hipMemcpyHostToDevice, c->stream));
             NCCL_TRY(ncclGroupStart());
             for (int d = 0; d < G; d++) {
@@ -828,151 +918,88 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                     NCCL_TRY(ncclRecv(c->inbox.p + roff[d] * rb, recv[d] * rb, ncclUint8, d, c->comm, c->stream));
             }
             NCCL_TRY(ncclGroupEnd());
-            const unsigned long long total = roff[G];
             for (int d = 0; d < G; d++)
-                if (d != c->shard)
-                    exchanged += (int64_t)send[d];
+                exchanged += (int64_t)send[d];
+            const unsigned long long total = roff[G];
             if (total) {
                 const unsigned long long blocks = std::min<unsigned long long>(4096, (total + kBlock - 1) / kBlock);
-                ops.insert_remote(dim3((unsigned)blocks), dim3(kBlock), c->stream, a, c->inbox.p, total);
+                ops.insert_remote(dim3((unsigned)blocks), blk, c->stream, a, c->inbox.p, total);
                 PA_TRY(check_launch());
             }
-        }
-        HIP_TRY(hipMemcpyAsync(c->h_stats, st, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
-        unsigned long long far_count = 0;
-        int goal_dev = kIntMax;
-        HIP_TRY(hipMemcpyAsync(&far_count, c->far_n.p, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(&goal_dev, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (cfg.profile && nb > 0) {
-            float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-            expand_ms += ms;
-        }
-        const StepStats &hs = *c->h_stats;
-        if (hs.overflow)
-            return fail(PASTAR_ENOMEM, "device capacity exhausted at step %lld (near %llu/%llu, far %llu/%llu, "
-                        "batch %llu, table 2^%d)", (long long)steps, hs.near_count, cfg.near_cap, far_count,
-                        cfg.far_cap, cfg.kmax, cfg.table_log2);
-        expanded += (int64_t)hs.expanded;
-        reopen += (int64_t)hs.reopen;
-        generated += (int64_t)hs.generated;
-        claimed += (int64_t)hs.claimed;
-        parents += (int64_t)nb;
-        cur = 1 - cur;
-        nn = hs.near_count;
-        nf = far_count;
-        base = new_base;
-        std::memcpy(hist.data(), hs.hist, sizeof(unsigned int) * kHistBins);
-        goal_g = goal_dev;
-        steps++;
-
-        // refill the near pile from the far pile (raise t_near)
-        if (nn < cfg.kmax && nf > 0) {
-            FarStats init{};
-            init.min_f = kIntMax;
-            HIP_TRY(hipMemcpyAsync(c->farstats.p, &init, sizeof(FarStats), hipMemcpyHostToDevice, c->stream));
-            const unsigned long long blocks = std::min<unsigned long long>(2048, (nf + kBlock - 1) / kBlock);
-            hipLaunchKernelGGL(far_min_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->far_buf[fcur].p, nf,
-                               goal_g, c->farstats.p);
-            PA_TRY(check_launch());
-            HIP_TRY(hipMemcpyAsync(c->h_far, c->farstats.p, sizeof(FarStats), hipMemcpyDeviceToHost, c->stream));
+            int goal_local = kIntMax;
+            HIP_TRY(hipMemcpyAsync(&goal_local, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
-            const int far_min = c->h_far->min_f;
-            if (c->h_far->live == 0) {
-                nf = 0;
-                HIP_TRY(hipMemsetAsync(c->far_n.p, 0, 8, c->stream));
-            } else {
-                if (nn == 0) {
-                    base = far_min;
-                    std::fill(hist.begin(), hist.end(), 0u);
-                }
-                const int cap_t = base + kHistBins - 1;
-                if (far_min < cap_t) {
-                    hipLaunchKernelGGL(far_hist_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream,
-                                       c->far_buf[fcur].p, nf, goal_g, far_min, c->farstats.p);
-                    PA_TRY(check_launch());
-                    HIP_TRY(hipMemcpyAsync(c->h_far, c->farstats.p, sizeof(FarStats), hipMemcpyDeviceToHost, c->stream));
-                    HIP_TRY(hipStreamSynchronize(c->stream));
-                    // enough entries for several steps, within the histogram window
-                    const unsigned long long want = 4 * cfg.kmax;
-                    unsigned long long cum = 0;
-                    int tn = cap_t;
-                    for (int b = 0; b < kHistBins - 1; b++) {
-                        cum += c->h_far->hist[b];
-                        if (cum >= want) {
-                            tn = far_min + b + 1;
-                            break;
-                        }
-                    }
-                    tn = std::min(tn, cap_t);
-                    StepStats *rs = c->stats.p + 2;
-                    HIP_TRY(hipMemsetAsync(rs, 0, sizeof(StepStats), c->stream));
-                    hipLaunchKernelGGL(far_partition_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream,
-                                       c->far_buf[fcur].p, nf, tn, goal_g, base, c->near_buf[cur].p + nn,
-                                       cfg.near_cap - nn, c->far_buf[1 - fcur].p, cfg.far_cap, rs);
-                    PA_TRY(check_launch());
-                    HIP_TRY(hipMemcpyAsync(c->h_stats, rs, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
-                    HIP_TRY(hipStreamSynchronize(c->stream));
-                    if (c->h_stats->overflow)
-                        return fail(PASTAR_ENOMEM, "near pile capacity exhausted during refill");
-                    nn += c->h_stats->near_count;
-                    nf = c->h_stats->far_count;
-                    for (int b = 0; b < kHistBins; b++)
-                        hist[b] += c->h_stats->hist[b];
-                    HIP_TRY(hipMemcpyAsync(c->far_n.p, &nf, 8, hipMemcpyHostToDevice, c->stream));
-                    fcur = 1 - fcur;
-                    t_near = tn;
-                }
-            }
-        }
-
-        // termination
-        if (G > 1) {
-            int64_t mn[1] = {goal_g};
+            h = *c->h_ctl;
+            // termination: no shard found a live bucket below the best goal
+            // in this step (then nothing was expanded or sent anywhere); a
+            // capacity failure on any shard stops every shard
+            int64_t mn[1] = {goal_local};
             PA_TRY(allreduce_i64(c, mn, 1, ncclMin));
-            goal_g = (int)mn[0];
-            HIP_TRY(hipMemcpyAsync(c->goal.p, &goal_g, 4, hipMemcpyHostToDevice, c->stream));
-            int64_t rem[1] = {(int64_t)(nn + nf)};
-            PA_TRY(allreduce_i64(c, rem, 1, ncclSum));
-            done = rem[0] == 0;
-        } else {
-            done = nn == 0 && nf == 0;
+            const int goal_g = (int)mn[0];
+            if (goal_g < goal_local)
+                HIP_TRY(hipMemcpy(c->goal.p, &goal_g, 4, hipMemcpyHostToDevice));
+            int64_t st2[2] = {had_work, h.status ? 1 : 0};
+            PA_TRY(allreduce_i64(c, st2, 2, ncclSum));
+            if (st2[1] != 0) {
+                if (!h.status) {
+                    c->last_fail_mask = 0;
+                    return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
+                }
+                break;
+            }
+            if (st2[0] == 0)
+                break;
+            if (cfg.verbose && h.steps % 50 == 0)
+                std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %llu bucket %d goal %d\n", c->shard, G,
+                             h.steps, h.expanded, h.cur_b, goal_g);
         }
-        if (cfg.verbose && (steps % 100 == 0 || done))
-            std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %lld near %llu far %llu goal %d base %d t_near %d\n",
-                         c->shard, G, (long long)steps, (long long)expanded, nn, nf, goal_g, base, t_near);
     }
     const double t1 = now_s();
+    if (h.status == 2) {
+        c->last_fail_mask = h.fail_mask;
+        return fail(PASTAR_ENOMEM, "device capacity exhausted (mask %d: pool %llu entries, sub-queue %llu entries, "
+                    "table 2^%d, outbox %llu)", h.fail_mask, cfg.pool_entries, cfg.subqueue_entries, cfg.table_log2,
+                    cfg.outbox_cap);
+    }
+    if (h.status == 3)
+        return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
+    int goal_g = kIntMax;
+    HIP_TRY(hipMemcpy(&goal_g, c->goal.p, 4, hipMemcpyDeviceToHost));
+    if (G > 1) {
+        int64_t mn[1] = {goal_g};
+        PA_TRY(allreduce_i64(c, mn, 1, ncclMin));
+        goal_g = (int)mn[0];
+    }
     if (goal_g == kIntMax)
         return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
 
-    // table census
+    // table and queue census
     DevBuf<unsigned long long> cnt;
-    PA_TRY(cnt.alloc(2));
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, 16, c->stream));
-    hipLaunchKernelGGL(count_table_kernel, dim3(2048), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
-                       slot_words_rt(c->kw), c->kw, cnt.p);
+    PA_TRY(cnt.alloc(3));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 24, c->stream));
+    hipLaunchKernelGGL(count_table_kernel, dim3(2048), blk, 0, c->stream, c->table.p, c->nslots, slot_words_rt(c->kw),
+                       c->kw, cnt.p);
+    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt.p + 2);
     PA_TRY(check_launch());
-    unsigned long long census[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(census, cnt.p, 16, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long census[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(census, cnt.p, 24, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
 
     std::memset(res, 0, sizeof(*res));
     res->score = goal_g;
-    res->expansions = expanded;
-    res->reopen = reopen;
-    res->generated = generated;
-    res->open_size = (int64_t)(nn + nf);
+    res->expansions = (int64_t)h.expanded;
+    res->reopen = (int64_t)h.reopen;
+    res->generated = (int64_t)h.generated;
+    res->open_size = (int64_t)census[2];
     res->closed_size = (int64_t)census[1];
     res->table_used = (int64_t)census[0];
-    res->steps = steps;
+    res->steps = h.steps;
     res->exchanged = exchanged;
     res->seconds = t1 - t0;
     res->expand_ms = expand_ms;
     res->expand_launches = launches;
-    res->expand_parents = parents;
-    int64_t all[1] = {expanded};
+    res->expand_parents = (int64_t)h.parents;
+    int64_t all[1] = {(int64_t)h.expanded};
     if (G > 1)
         PA_TRY(allreduce_i64(c, all, 1, ncclSum));
     // the goal's acceptance counts as one expansion (PAStar.cpp:341)
@@ -998,24 +1025,68 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         o = *opts;
     SearchCfg cfg;
     const unsigned long long masks = (1ull << c->n) - 1;
-    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 8192ull;
-    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 24;
+    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 32768ull;
+    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 22;
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
-    cfg.near_cap = o.near_capacity > 0 ? (unsigned long long)o.near_capacity
-                                       : std::max<unsigned long long>(1ull << 22, 2 * cfg.kmax * masks);
-    cfg.far_cap = o.far_capacity > 0 ? (unsigned long long)o.far_capacity : (1ull << 24);
-    cfg.outbox_cap = cfg.kmax * masks;
+    cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 24);
+    cfg.subqueue_entries = o.subqueue_entries > 0 ? (unsigned long long)o.subqueue_entries : (1ull << 20);
+    cfg.outbox_cap = std::max<unsigned long long>(1ull << 16, cfg.kmax * masks / std::max(1, c->n_shards));
+    cfg.table_log2 = std::max(cfg.table_log2, c->grown_log2);
+    cfg.pool_entries = std::max(cfg.pool_entries, c->grown_pool);
+    cfg.subqueue_entries = std::max(cfg.subqueue_entries, c->grown_maxch * (unsigned long long)kChunk);
+    cfg.outbox_cap = std::max(cfg.outbox_cap, c->grown_outbox);
     cfg.verbose = o.verbose;
     cfg.profile = o.profile;
+    cfg.eager = o.eager;
+    cfg.band = o.band;
     cfg.max_steps = o.max_steps;
-    int rc;
-    if (c->kw == 1)
-        rc = search_impl<1>(c, cfg, res);
-    else if (c->kw == 2)
-        rc = search_impl<2>(c, cfg, res);
-    else
-        rc = search_impl<4>(c, cfg, res);
+    int rc = PASTAR_OK, retries = 0;
+    for (;;) {
+        c->last_fail_mask = 0;
+        if (c->kw == 1)
+            rc = search_impl<1>(c, cfg, res);
+        else if (c->kw == 2)
+            rc = search_impl<2>(c, cfg, res);
+        else
+            rc = search_impl<4>(c, cfg, res);
+        if (rc != PASTAR_ENOMEM || o.no_autogrow || retries >= 8)
+            break;
+        int mask = c->last_fail_mask;
+        if (c->n_shards > 1) {  // every shard grows the same way
+            int64_t bits[4] = {mask & 1, (mask >> 1) & 1, (mask >> 2) & 1, (mask >> 3) & 1};
+            const std::string err = g_err;
+            if (allreduce_i64(c, bits, 4, ncclSum) != PASTAR_OK)
+                break;
+            g_err = err;
+            mask = (bits[0] ? 1 : 0) | (bits[1] ? 2 : 0) | (bits[2] ? 4 : 0) | (bits[3] ? 8 : 0);
+        }
+        if (!mask)
+            break;
+        if (mask & kFailNear)
+            cfg.pool_entries *= 4;
+        if (mask & kFailFar)
+            cfg.subqueue_entries *= 4;
+        if (mask & kFailTable)
+            cfg.table_log2 = std::min(32, cfg.table_log2 + 2);
+        if (mask & kFailOut)
+            cfg.outbox_cap *= 4;
+        c->grown_pool = cfg.pool_entries;
+        c->grown_maxch = maxch_of(cfg);
+        c->grown_log2 = cfg.table_log2;
+        c->grown_outbox = cfg.outbox_cap;
+        retries++;
+        if (cfg.verbose)
+            std::fprintf(stderr, "[pastar] capacity grow (mask %d): pool %llu sub-queue %llu table 2^%d outbox %llu\n",
+                         mask, cfg.pool_entries, cfg.subqueue_entries, cfg.table_log2, cfg.outbox_cap);
+    }
+    if (rc == PASTAR_OK) {
+        res->capacity_retries = retries;
+        res->table_slots = (int64_t)c->nslots;
+        res->pool_entries = (int64_t)cfg.pool_entries;
+        res->subqueue_entries = (int64_t)cfg.subqueue_entries;
+        res->graph_replay = c->graph_used ? 1 : 0;
+    }
     return rc;
 }
 

@@ -118,15 +118,20 @@ class PAStarOpt:
     threads_num: int = 1
     batch_nodes: int = 0
     table_slots_log2: int = 0
-    near_capacity: int = 0
-    far_capacity: int = 0
+    pool_entries: int = 0
+    subqueue_entries: int = 0
     max_steps: int = 0
+    band: int = 0
     profile: bool = False
     verbose: bool = False
+    autogrow: bool = True
+    eager: bool = False
 
     def search_opts(self):
-        return nat.pastar_search_opts(self.batch_nodes, self.table_slots_log2, self.near_capacity,
-                                      self.far_capacity, self.max_steps, int(self.profile), int(self.verbose))
+        return nat.pastar_search_opts(self.batch_nodes, self.table_slots_log2, self.pool_entries,
+                                      self.subqueue_entries, self.max_steps, self.band, int(self.profile),
+                                      int(self.verbose),
+                                      int(not self.autogrow), int(self.eager))
 
 
 def compute_weights(seqs):
@@ -161,6 +166,11 @@ class SearchResult:
     expand_ms: float
     expand_launches: int
     expand_parents: int
+    capacity_retries: int = 0
+    table_slots: int = 0
+    pool_entries: int = 0
+    subqueue_entries: int = 0
+    graph_replay: int = 0
     extra: dict = field(default_factory=dict)
 
 

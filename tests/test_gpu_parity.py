@@ -83,11 +83,13 @@ def test_get_neigh_matches_oracle(name, vec_size, hash_type, shift, kat, oracles
 
 
 @pytest.mark.parametrize("name", SMALL)
-@pytest.mark.parametrize("batch", [0, 1, 64])
-def test_search_score_bit_exact(name, batch, kat, oracles):
+@pytest.mark.parametrize("batch,eager", [(0, False), (1, False), (64, False), (0, True)])
+def test_search_score_bit_exact(name, batch, eager, kat, oracles):
     ref = kat["inputs"][name]
     with _engine(name, kat) as e:
-        r = e.pa_star(PAStarOpt(batch_nodes=batch))
+        r = e.pa_star(PAStarOpt(batch_nodes=batch, eager=eager, profile=True))
+        assert r.graph_replay == (0 if eager else 1)
+        assert r.expand_ms > 0
         assert r.score == ref["score"]
         rows = e.alignment()
         # the backtrace is a real alignment whose SP cost is the score
@@ -106,7 +108,7 @@ def test_search_score_bit_exact(name, batch, kat, oracles):
 def test_search_kinase(kat, oracles):
     ref = kat["inputs"]["kinase"]
     with _engine("kinase", kat) as e:
-        r = e.pa_star(PAStarOpt(table_slots_log2=26, far_capacity=1 << 26))
+        r = e.pa_star(PAStarOpt(table_slots_log2=26))
         assert r.score == ref["score"]
         rows = e.alignment()
         assert oracles["kinase"].alignment_cost(rows) == ref["score"]
@@ -119,7 +121,7 @@ def test_search_n8(name, kat):
     seqs = Sequences.from_fasta(golden(ref["file"]))
     o = orc.Oracle(fasta=golden(ref["file"]))
     with Engine(seqs).init() as e:
-        r = e.pa_star(PAStarOpt(table_slots_log2=27, far_capacity=1 << 27))
+        r = e.pa_star(PAStarOpt(table_slots_log2=27))
         assert r.score == ref["score"]
         rows = e.alignment()
         assert o.alignment_cost(rows) == ref["score"]
@@ -139,3 +141,16 @@ def test_random_small_problems_match_oracle():
             assert r.score == ref["score"], (seqs, r, ref)
             rows = e.alignment()
             assert o.alignment_cost(rows) == ref["score"]
+
+
+def test_capacity_autogrow(kat):
+    """Starting from tiny capacities the engine grows the exhausted buffer and
+    restarts; the result is unchanged."""
+    ref = kat["inputs"]["syn4x200_s1"]
+    with _engine("syn4x200_s1", kat) as e:
+        r = e.pa_star(PAStarOpt(table_slots_log2=10, pool_entries=4096, subqueue_entries=4096, batch_nodes=64))
+        assert r.score == ref["score"]
+        assert r.capacity_retries > 0
+        with pytest.raises(Exception):
+            e2 = Engine(e.sequences).init()
+            e2.pa_star(PAStarOpt(table_slots_log2=10, pool_entries=4096, autogrow=False))
