@@ -160,6 +160,16 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
                       const void *rccl_id, pastar_ctx **out);
 void pastar_gpu_destroy(pastar_ctx *ctx);
 
+/* In-process shard group: n_shards contexts in one process, each driven by
+ * its own host thread (pastar_gpu_search is collective over the group);
+ * nodes move between shards by peer copies instead of RCCL.  The shards may
+ * share one device (the sharded path on a single GPU) or use several. */
+typedef struct pastar_group pastar_group;
+int pastar_group_create(int n_shards, pastar_group **out);
+void pastar_group_destroy(pastar_group *group); /* after its contexts */
+int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group *group, int shard_rank,
+                              pastar_ctx **out);
+
 /* Phase 1: PairAlign tables by the anti-diagonal wavefront kernel. */
 int pastar_gpu_build_heuristic(pastar_ctx *ctx);
 int pastar_gpu_pair_table(pastar_ctx *ctx, int pair, int32_t *out);

@@ -7,7 +7,7 @@ include/pastar_gpu.h.  This package is the Python host mirror of the
 reference interface; see pastar.py.
 """
 from .pastar import (Engine, Node, PAStarOpt, SearchResult, Sequences, compute_weights, cost, get_id,
-                     rccl_unique_id, similarity)
+                     rccl_unique_id, sharded_search, similarity, ShardGroup)
 
 __all__ = ["Engine", "Node", "PAStarOpt", "SearchResult", "Sequences", "compute_weights", "cost", "get_id",
-           "rccl_unique_id", "similarity"]
+           "rccl_unique_id", "sharded_search", "similarity", "ShardGroup"]

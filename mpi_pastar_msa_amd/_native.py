@@ -97,6 +97,10 @@ SIGNATURES = {
     "pastar_gpu_create": (ctypes.c_int, [ctypes.POINTER(pastar_problem), ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "pastar_gpu_destroy": (None, [ctypes.c_void_p]),
+    "pastar_group_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "pastar_group_destroy": (None, [ctypes.c_void_p]),
+    "pastar_gpu_create_grouped": (ctypes.c_int, [ctypes.POINTER(pastar_problem), ctypes.c_int, ctypes.c_void_p,
+                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "pastar_gpu_build_heuristic": (ctypes.c_int, [ctypes.c_void_p]),
     "pastar_gpu_pair_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]),
     "pastar_gpu_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),

@@ -319,8 +319,12 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
         const int bl = __shfl(b, leader);
         const uint64_t m = __ballot(pred && b == bl) & pending;
         unsigned long long base = 0;
-        if (lane == leader)
+        if (lane == leader) {
             base = atomicAdd(&a.q->W[bl][sq], (unsigned long long)__popcll(m));
+            // entries from other shards may land below this shard's minimum
+            if (bl < a.ctl->cur_b)
+                atomicMin(&a.ctl->cur_b, bl);
+        }
         base = __shfl(base, leader);
         if ((m >> lane) & 1ull)
             queue_store(a, bl, sq, base + __popcll(m & ((1ull << lane) - 1ull)), e, st);
@@ -425,7 +429,6 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         if (tid == 0) {
             ctl->n_batch = 0;
             ctl->has_work = 0;
-            ctl->cur_b = limit + 1 < kBuckets ? limit + 1 : kBuckets - 1;
             if (ctl->n_shards == 1)
                 ctl->status = 1;
             ctl->steps++;

@@ -16,7 +16,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -103,11 +107,134 @@ double now_s()
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// ---------------------------------------------------------------------------
+// Shard transports.  The search talks to the other shards through four
+// operations; RCCL implements them for one process per GPU (the reference's
+// MPI ranks), LocalGroup for several shards driven by threads of one process
+// (peer copies; also how the sharded path is tested on a single GPU).
+// ---------------------------------------------------------------------------
+enum RedOp { kRedSum, kRedMin };
+
+struct Transport {
+    virtual ~Transport() = default;
+    // element-wise reduction of host int64 values over all shards
+    virtual int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) = 0;
+    // send[d] records go to shard d; recv[s] arrive from shard s
+    virtual int exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv) = 0;
+    // outbox segment d -> inbox of shard d at that shard's roff[me]
+    virtual int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
+                                 const unsigned long long *roff, size_t rb, size_t outbox_cap) = 0;
+    // device buffer of `root` copied to every shard's same buffer
+    virtual int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) = 0;
+};
+
+}  // namespace
+
+struct pastar_group {
+    int G = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long long gen = 0;
+    bool broken = false;
+    std::vector<std::array<int64_t, 8>> vals;
+    std::vector<std::vector<unsigned long long>> counts;
+    std::vector<const uint8_t *> outbox;
+    std::vector<void *> bufs;
+    std::vector<int> device;
+    std::atomic<int> members{0};
+
+    // returns false when the group is broken (a member failed) or on timeout
+    bool barrier()
+    {
+        std::unique_lock<std::mutex> l(mu);
+        if (broken)
+            return false;
+        const long long g = gen;
+        if (++arrived == G) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(l, std::chrono::seconds(600), [&] { return gen != g || broken; });
+        if (!ok || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+    void breakdown()
+    {
+        std::lock_guard<std::mutex> l(mu);
+        broken = true;
+        cv.notify_all();
+    }
+};
+
+namespace {
+
+class LocalTransport : public Transport {
+   public:
+    LocalTransport(pastar_group *g, int rank) : g_(g), rank_(rank) {}
+    ~LocalTransport() override { g_->members--; }
+
+    int sync()
+    {
+        if (!g_->barrier())
+            return fail(PASTAR_ECOMM, "shard group broken (a shard failed or timed out)");
+        return PASTAR_OK;
+    }
+    int allreduce(pastar_ctx *, int64_t *vals, int count, RedOp op) override
+    {
+        for (int k = 0; k < count; k++)
+            g_->vals[rank_][k] = vals[k];
+        PA_TRY(sync());
+        for (int k = 0; k < count; k++) {
+            int64_t r = g_->vals[0][k];
+            for (int s = 1; s < g_->G; s++)
+                r = op == kRedSum ? r + g_->vals[s][k] : std::min(r, g_->vals[s][k]);
+            vals[k] = r;
+        }
+        return sync();
+    }
+    int exchange_counts(pastar_ctx *, const unsigned long long *send, unsigned long long *recv) override
+    {
+        g_->counts[rank_].assign(send, send + g_->G);
+        PA_TRY(sync());
+        for (int s = 0; s < g_->G; s++)
+            recv[s] = g_->counts[s][rank_];
+        return sync();
+    }
+    int exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
+                         const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
+    int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
+
+   private:
+    pastar_group *g_;
+    int rank_;
+};
+
+class RcclTransport : public Transport {
+   public:
+    explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
+    ~RcclTransport() override { ncclCommDestroy(comm_); }
+    int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) override;
+    int exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv) override;
+    int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
+                         const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
+    int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
+
+   private:
+    ncclComm_t comm_;
+};
+
 }  // namespace
 
 struct pastar_ctx {
     int device = 0, n_shards = 1, shard = 0;
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Transport> tr;  // set when n_shards > 1
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
@@ -452,7 +579,9 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
             return fail(PASTAR_EINVAL, "rccl_id required for n_shards > 1");
         ncclUniqueId id;
         std::memcpy(&id, rccl_id, sizeof(id));
-        NCCL_TRY(ncclCommInitRank(&c->comm, n_shards, id, shard_rank));
+        ncclComm_t comm = nullptr;
+        NCCL_TRY(ncclCommInitRank(&comm, n_shards, id, shard_rank));
+        c->tr.reset(new RcclTransport(comm));
     }
     HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
@@ -467,8 +596,7 @@ void pastar_gpu_destroy(pastar_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
-    if (c->comm)
-        ncclCommDestroy(c->comm);
+    c->tr.reset();
     if (c->h_stats)
         (void)hipHostFree(c->h_stats);
     if (c->h_ctl)
@@ -661,15 +789,9 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     return PASTAR_OK;
 }
 
-int allreduce_i64(pastar_ctx *c, int64_t *vals, int count, ncclRedOp_t op)
+int allreduce_i64(pastar_ctx *c, int64_t *vals, int count, RedOp op)
 {
-    DevBuf<int64_t> d;
-    PA_TRY(d.alloc((size_t)count));
-    HIP_TRY(hipMemcpyAsync(d.p, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
-    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, op, c->comm, c->stream));
-    HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return PASTAR_OK;
+    return c->tr->allreduce(c, vals, count, op);
 }
 
 // Bucket width (the band of f one step expands).  Default: about a third of
@@ -895,29 +1017,11 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             for (int d = 0; d < G; d++)
                 send[d] = std::min<unsigned long long>(c->h_stats->outbox_count[d], cfg.outbox_cap);
             send[c->shard] = 0;
-            HIP_TRY(hipMemcpyAsync(c->xcounts.p, send.data(), 8 * G, hipMemcpyHostToDevice, c->stream));
-            NCCL_TRY(ncclGroupStart());
-            for (int d = 0; d < G; d++) {
-                NCCL_TRY(ncclSend(c->xcounts.p + d, 1, ncclUint64, d, c->comm, c->stream));
-                NCCL_TRY(ncclRecv(c->xcounts.p + G + d, 1, ncclUint64, d, c->comm, c->stream));
-            }
-            NCCL_TRY(ncclGroupEnd());
-            HIP_TRY(hipMemcpyAsync(recv.data(), c->xcounts.p + G, 8 * G, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
+            PA_TRY(c->tr->exchange_counts(c, send.data(), recv.data()));
             std::vector<unsigned long long> roff(G + 1, 0);
             for (int d = 0; d < G; d++)
                 roff[d + 1] = roff[d] + recv[d];
-            NCCL_TRY(ncclGroupStart());
-            for (int d = 0; d < G; d++) {
-                if (d == c->shard)
-                    continue;
-                if (send[d])
-                    NCCL_TRY(ncclSend(c->outbox.p + (size_t)d * cfg.outbox_cap * rb, send[d] * rb, ncclUint8, d,
-                                      c->comm, c->stream));
-                if (recv[d])
-                    NCCL_TRY(ncclRecv(c->inbox.p + roff[d] * rb, recv[d] * rb, ncclUint8, d, c->comm, c->stream));
-            }
-            NCCL_TRY(ncclGroupEnd());
+            PA_TRY(c->tr->exchange_records(c, send.data(), recv.data(), roff.data(), rb, cfg.outbox_cap));
             for (int d = 0; d < G; d++)
                 exchanged += (int64_t)send[d];
             const unsigned long long total = roff[G];
@@ -934,12 +1038,12 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             // in this step (then nothing was expanded or sent anywhere); a
             // capacity failure on any shard stops every shard
             int64_t mn[1] = {goal_local};
-            PA_TRY(allreduce_i64(c, mn, 1, ncclMin));
+            PA_TRY(allreduce_i64(c, mn, 1, kRedMin));
             const int goal_g = (int)mn[0];
             if (goal_g < goal_local)
                 HIP_TRY(hipMemcpy(c->goal.p, &goal_g, 4, hipMemcpyHostToDevice));
             int64_t st2[2] = {had_work, h.status ? 1 : 0};
-            PA_TRY(allreduce_i64(c, st2, 2, ncclSum));
+            PA_TRY(allreduce_i64(c, st2, 2, kRedSum));
             if (st2[1] != 0) {
                 if (!h.status) {
                     c->last_fail_mask = 0;
@@ -967,7 +1071,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     HIP_TRY(hipMemcpy(&goal_g, c->goal.p, 4, hipMemcpyDeviceToHost));
     if (G > 1) {
         int64_t mn[1] = {goal_g};
-        PA_TRY(allreduce_i64(c, mn, 1, ncclMin));
+        PA_TRY(allreduce_i64(c, mn, 1, kRedMin));
         goal_g = (int)mn[0];
     }
     if (goal_g == kIntMax)
@@ -1001,7 +1105,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     res->expand_parents = (int64_t)h.parents;
     int64_t all[1] = {(int64_t)h.expanded};
     if (G > 1)
-        PA_TRY(allreduce_i64(c, all, 1, ncclSum));
+        PA_TRY(allreduce_i64(c, all, 1, kRedSum));
     // the goal's acceptance counts as one expansion (PAStar.cpp:341)
     res->expansions_all = all[0] + 1;
     c->searched = true;
@@ -1056,7 +1160,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         if (c->n_shards > 1) {  // every shard grows the same way
             int64_t bits[4] = {mask & 1, (mask >> 1) & 1, (mask >> 2) & 1, (mask >> 3) & 1};
             const std::string err = g_err;
-            if (allreduce_i64(c, bits, 4, ncclSum) != PASTAR_OK)
+            if (allreduce_i64(c, bits, 4, kRedSum) != PASTAR_OK)
                 break;
             g_err = err;
             mask = (bits[0] ? 1 : 0) | (bits[1] ? 2 : 0) | (bits[2] ? 4 : 0) | (bits[3] ? 8 : 0);
@@ -1167,13 +1271,13 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
                 return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d)", info[0], info[1]);
         }
         if (G > 1) {
-            NCCL_TRY(ncclBroadcast(dinfo.p, dinfo.p, 2, ncclInt32, owner, c->comm, c->stream));
+            PA_TRY(c->tr->broadcast(c, dinfo.p, 8, owner));
             HIP_TRY(hipMemcpyAsync(info, dinfo.p, 8, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             if (info[1] < 0 || info[1] == 2)
                 return fail(PASTAR_ENOTFOUND, "backtrace broken on shard %d", owner);
             if (info[0] > 0)
-                NCCL_TRY(ncclBroadcast(dmasks.p, dmasks.p, (size_t)info[0], ncclInt32, owner, c->comm, c->stream));
+                PA_TRY(c->tr->broadcast(c, dmasks.p, 4 * (size_t)info[0], owner));
         }
         seg.resize((size_t)info[0]);
         if (info[0] > 0)
@@ -1201,6 +1305,142 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
     for (int i = 0; i < c->n; i++)
         rows[(size_t)i * stride + L] = '\0';
     *cols = L;
+    return PASTAR_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Transport implementations
+// ---------------------------------------------------------------------------
+namespace {
+
+int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
+{
+    DevBuf<int64_t> d;
+    PA_TRY(d.alloc((size_t)count));
+    HIP_TRY(hipMemcpyAsync(d.p, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
+    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, op == kRedSum ? ncclSum : ncclMin, comm_, c->stream));
+    HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
+int RcclTransport::exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv)
+{
+    const int G = c->n_shards;
+    HIP_TRY(hipMemcpyAsync(c->xcounts.p, send, 8 * G, hipMemcpyHostToDevice, c->stream));
+    NCCL_TRY(ncclGroupStart());
+    for (int d = 0; d < G; d++) {
+        NCCL_TRY(ncclSend(c->xcounts.p + d, 1, ncclUint64, d, comm_, c->stream));
+        NCCL_TRY(ncclRecv(c->xcounts.p + G + d, 1, ncclUint64, d, comm_, c->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipMemcpyAsync(recv, c->xcounts.p + G, 8 * G, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
+int RcclTransport::exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
+                                    const unsigned long long *roff, size_t rb, size_t outbox_cap)
+{
+    NCCL_TRY(ncclGroupStart());
+    for (int d = 0; d < c->n_shards; d++) {
+        if (d == c->shard)
+            continue;
+        if (send[d])
+            NCCL_TRY(ncclSend(c->outbox.p + (size_t)d * outbox_cap * rb, send[d] * rb, ncclUint8, d, comm_, c->stream));
+        if (recv[d])
+            NCCL_TRY(ncclRecv(c->inbox.p + roff[d] * rb, recv[d] * rb, ncclUint8, d, comm_, c->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return PASTAR_OK;
+}
+
+int RcclTransport::broadcast(pastar_ctx *c, void *dev, size_t bytes, int root)
+{
+    NCCL_TRY(ncclBroadcast(dev, dev, bytes, ncclUint8, root, comm_, c->stream));
+    return PASTAR_OK;
+}
+
+int LocalTransport::exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
+                                     const unsigned long long *roff, size_t rb, size_t outbox_cap)
+{
+    g_->outbox[rank_] = c->outbox.p;
+    g_->device[rank_] = c->device;
+    PA_TRY(sync());
+    for (int s = 0; s < g_->G; s++) {
+        if (s == rank_ || !recv[s])
+            continue;
+        const uint8_t *src = g_->outbox[s] + (size_t)rank_ * outbox_cap * rb;
+        HIP_TRY(hipMemcpyPeerAsync(c->inbox.p + roff[s] * rb, c->device, src, g_->device[s], recv[s] * rb, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return sync();  // peers may refill their outboxes only after every copy
+}
+
+int LocalTransport::broadcast(pastar_ctx *c, void *dev, size_t bytes, int root)
+{
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    g_->bufs[rank_] = dev;
+    g_->device[rank_] = c->device;
+    PA_TRY(sync());
+    if (rank_ != root) {
+        HIP_TRY(hipMemcpyPeerAsync(dev, c->device, g_->bufs[root], g_->device[root], bytes, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return sync();
+}
+
+}  // namespace
+
+extern "C" {
+
+int pastar_group_create(int n_shards, pastar_group **out)
+{
+    if (!out || n_shards < 1 || n_shards > 8)
+        return fail(PASTAR_EINVAL, "invalid group size %d (1..8)", n_shards);
+    pastar_group *g = new pastar_group();
+    g->G = n_shards;
+    g->vals.resize(n_shards);
+    g->counts.resize(n_shards);
+    g->outbox.resize(n_shards, nullptr);
+    g->bufs.resize(n_shards, nullptr);
+    g->device.resize(n_shards, 0);
+    *out = g;
+    return PASTAR_OK;
+}
+
+void pastar_group_destroy(pastar_group *g)
+{
+    delete g;
+}
+
+int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group *group, int shard_rank,
+                              pastar_ctx **out)
+{
+    if (!group || !out)
+        return fail(PASTAR_EINVAL, "null argument");
+    if (shard_rank < 0 || shard_rank >= group->G)
+        return fail(PASTAR_EINVAL, "shard %d outside group of %d", shard_rank, group->G);
+    // a context with one shard, then joined to the group
+    PA_TRY(pastar_gpu_create(p, device, 1, 0, nullptr, out));
+    pastar_ctx *c = *out;
+    c->n_shards = group->G;
+    c->shard = shard_rank;
+    c->hp.n_shards = group->G;
+    c->hp.shard = shard_rank;
+    HIP_TRY(hipMemcpy(c->dP.p, &c->hp, sizeof(c->hp), hipMemcpyHostToDevice));
+    if (group->G > 1) {
+        c->tr.reset(new LocalTransport(group, shard_rank));
+        group->members++;
+        for (int d = 0; d < 8; d++) {  // peer access for the copies, where the link allows it
+            int ok = 0;
+            if (d != device && hipDeviceCanAccessPeer(&ok, device, d) == hipSuccess && ok)
+                (void)hipDeviceEnablePeerAccess(d, 0);
+        }
+        (void)hipGetLastError();
+    }
     return PASTAR_OK;
 }
 

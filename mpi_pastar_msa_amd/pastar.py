@@ -174,12 +174,27 @@ class SearchResult:
     extra: dict = field(default_factory=dict)
 
 
+class ShardGroup:
+    """In-process shard group (pastar_group_create): several Engines driven by
+    threads of one process exchange nodes by peer copies instead of RCCL."""
+
+    def __init__(self, n_shards):
+        self.n_shards = n_shards
+        self._g = ctypes.c_void_p()
+        check(lib().pastar_group_create(n_shards, ctypes.byref(self._g)))
+
+    def close(self):
+        if self._g:
+            lib().pastar_group_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+
 class Engine:
     """One device context (one GPU shard).  Owns the device memory."""
 
     def __init__(self, sequences, device=0, n_shards=1, shard_rank=0, rccl_id=None, weights=None,
                  hash_type="FZORDER", hash_shift=12, gap_open=GAP_OPEN, gap_ext=GAP_EXTENSION,
-                 gap_gap=GAP_GAP):
+                 gap_gap=GAP_GAP, group=None):
         if isinstance(sequences, (list, tuple)):
             sequences = Sequences(sequences)
         if not 0 <= hash_shift <= 21:
@@ -200,8 +215,13 @@ class Engine:
                                   self._w if self._w is not None else None, None,
                                   gap_open, gap_ext, gap_gap, ht, hash_shift)
         self._ctx = ctypes.c_void_p()
-        check(lib().pastar_gpu_create(ctypes.byref(prob), device, n_shards, shard_rank, rccl_id,
-                                      ctypes.byref(self._ctx)))
+        if group is not None:
+            self.n_shards = group.n_shards
+            check(lib().pastar_gpu_create_grouped(ctypes.byref(prob), device, group._g, shard_rank,
+                                                  ctypes.byref(self._ctx)))
+        else:
+            check(lib().pastar_gpu_create(ctypes.byref(prob), device, n_shards, shard_rank, rccl_id,
+                                          ctypes.byref(self._ctx)))
         self.npairs = npairs
         self.pairs = [(x, y) for x in range(self.n - 1) for y in range(x + 1, self.n)]
         self._ready = False
@@ -319,6 +339,38 @@ class Engine:
         check(lib().pastar_gpu_alignment(self._ctx, buf, stride, ctypes.byref(cols)))
         raw = buf.raw
         return [raw[i * stride:i * stride + cols.value].decode("latin-1") for i in range(self.n)]
+
+
+def sharded_search(sequences, n_shards, devices=(0,), opt=None, **engine_kw):
+    """One search sharded over `n_shards` contexts of this process (one host
+    thread each, ShardGroup transport); devices are used round-robin.
+    Returns (per-shard SearchResult list, alignment rows)."""
+    import threading
+    if isinstance(sequences, (list, tuple)):
+        sequences = Sequences(sequences)
+    group = ShardGroup(n_shards)
+    engines = [Engine(sequences, device=devices[r % len(devices)], shard_rank=r, group=group, **engine_kw)
+               for r in range(n_shards)]
+    results, rows, errors = [None] * n_shards, [None] * n_shards, []
+
+    def run(r):
+        try:
+            results[r] = engines[r].pa_star(opt)
+            rows[r] = engines[r].alignment()
+        except Exception as ex:  # pragma: no cover - surfaced below
+            errors.append(ex)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(n_shards)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for e in engines:
+        e.close()
+    group.close()
+    if errors:
+        raise errors[0]
+    return results, rows[0]
 
 
 def similarity(rows):

@@ -154,3 +154,23 @@ def test_capacity_autogrow(kat):
         with pytest.raises(Exception):
             e2 = Engine(e.sequences).init()
             e2.pa_star(PAStarOpt(table_slots_log2=10, pool_entries=4096, autogrow=False))
+
+
+@pytest.mark.parametrize("name,shards", [("test2", 2), ("PF08184", 3), ("syn4x200_s1", 2), ("syn4x200_s1", 4),
+                                          ("kinase", 4), ("syn8x100_s3", 8)])
+def test_sharded_search_one_gpu(name, shards, kat, oracles):
+    """The multi-shard path (z-order owner routing, record exchange, global
+    termination, cross-shard backtrace) with an in-process shard group on one
+    device: same optimal score, a valid optimal alignment."""
+    from mpi_pastar_msa_amd import sharded_search
+    ref = kat["inputs"][name]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    res, rows = sharded_search(seqs, shards, opt=PAStarOpt(batch_nodes=4096))
+    assert all(r.score == ref["score"] for r in res)
+    assert len({r.expansions_all for r in res}) == 1
+    assert sum(r.expansions for r in res) + 1 == res[0].expansions_all
+    assert sum(r.exchanged for r in res) > 0
+    o = oracles[name] if name in oracles else orc.Oracle(fasta=golden(ref["file"]))
+    assert o.alignment_cost(rows) == ref["score"]
+    if "alignment_md5" in ref:
+        assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
