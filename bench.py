@@ -9,13 +9,31 @@ region; contexts and device buffers are created before it too.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
 
-N > 1 runs one rank per GPU (torch.distributed.run); the ranks shard one
-search by the reference's z-order owner hash and exchange nodes over RCCL
-(strong scaling: the total work is one search).  Rank 0 prints one JSON line.
+N > 1 runs one rank per GPU (launched by torch.distributed.run, which sets
+RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT); the ranks shard one search by
+the reference's z-order owner hash and exchange nodes over RCCL (strong
+scaling: the total work is one search).  Rank 0 prints one JSON line.
+
+The timed region is bracketed by a barrier and a device synchronize on both
+sides and the time is the max over ranks, as the driver contract asks; both go
+through the engine (RCCL allreduce, hipDeviceSynchronize) rather than
+torch.distributed / torch.cuda: importing torch in this process would load
+torch's bundled ROCm 7.0 HIP runtime in place of the system 7.2 one, under
+which hipGraph capture of the step loop with event nodes is refused.  The
+RCCL unique id is handed from rank 0 to the others over a TCP socket on
+MASTER_PORT + 17.
+
+Roofline: the expand kernel's average launch duration is measured live in the
+timed region by the kernel itself (first-block start to last-block end on the
+100 MHz device clock, accumulated on the device; PAStarOpt.profile), because
+HIP event nodes inside the replayed graph cost several microseconds per step;
+profiles/ holds the rocprofv3 kernel-trace summary of the same command for the
+cross-check.
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -72,6 +90,40 @@ def cpu_baseline(fasta, budget_s):
             "wall_to_optimal_s": secs / runs, "score": r["score"]}
 
 
+def share_rccl_id(rank, world, make_id):
+    """Rank 0 creates the RCCL unique id and sends it to every other rank."""
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 17
+    if rank == 0:
+        rid = make_id()
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        srv.bind(("", port))
+        srv.listen(world)
+        srv.settimeout(300)
+        for _ in range(world - 1):
+            conn, _ = srv.accept()
+            conn.sendall(rid)
+            conn.close()
+        srv.close()
+        return rid
+    deadline = time.time() + 300
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=10) as c:
+                buf = b""
+                while len(buf) < 128:
+                    chunk = c.recv(128 - len(buf))
+                    if not chunk:
+                        raise ConnectionError("short read")
+                    buf += chunk
+                return buf
+        except OSError:
+            if time.time() > deadline:
+                raise
+            time.sleep(0.2)
+
+
 def pmc_traffic(workload):
     """HBM bytes per expand launch from a committed rocprofv3 PMC summary of
     the same workload (profiles/pmc_<workload>.json, tools/pmc_summary.py)."""
@@ -105,24 +157,17 @@ def main():
             sys.exit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
         args.gpus = world
 
-    import torch
-    import torch.distributed as dist
     from mpi_pastar_msa_amd import Engine, PAStarOpt, Sequences, rccl_unique_id
 
     dist_on = world > 1
-    if dist_on:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    rid = None
-    if dist_on:
-        box = [rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        rid = box[0]
+    rid = share_rccl_id(rank, world, rccl_unique_id) if dist_on else None
 
     fasta_name, cfg_desc, known = WORKLOADS[args.workload]
     fasta = os.path.join(GOLDEN, fasta_name)
     seqs = Sequences.from_fasta(fasta)
     n = len(seqs.seqs)
-    engine = Engine(seqs, device=local_rank, n_shards=world, shard_rank=rank, rccl_id=rid)
+    device = env_int("PASTAR_BENCH_DEVICE", local_rank)  # override for single-GPU rehearsals
+    engine = Engine(seqs, device=device, n_shards=world, shard_rank=rank, rccl_id=rid)
     opt = PAStarOpt(batch_nodes=args.batch, table_slots_log2=args.table_log2,
                     pool_entries=args.pool, band=args.band, profile=True)
 
@@ -135,18 +180,14 @@ def main():
     for _ in range(args.warmup):
         step()
 
-    def barrier():
-        if dist_on:
-            dist.barrier()
-
     results = []
-    barrier()
-    torch.cuda.synchronize()
+    engine.barrier()
+    engine.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         results.append(step())
-    torch.cuda.synchronize()
-    barrier()
+    engine.synchronize()
+    engine.barrier()
     elapsed = time.perf_counter() - t0
 
     exp_all = sum(r.expansions_all for r, _ in results)
@@ -155,15 +196,13 @@ def main():
     launches = sum(r.expand_launches for r, _ in results)
     wall = sum(r.seconds for r, _ in results) / len(results)
     score = results[-1][0].score
-    if dist_on:
-        t = torch.tensor([elapsed, wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, wall = float(t[0]), float(t[1])
+    if dist_on:  # max over ranks (ns resolution)
+        mx = engine.allreduce([int(elapsed * 1e9), int(wall * 1e9)], "max")
+        elapsed, wall = mx[0] / 1e9, mx[1] / 1e9
         # the roofline is reported for rank 0's expand kernel
     if rank != 0:
-        if dist_on:
-            dist.barrier()
-            dist.destroy_process_group()
+        engine.barrier()
+        engine.close()
         return
 
     value = exp_all / elapsed
@@ -205,9 +244,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fasta, args.cpu_seconds)
     print(json.dumps(line), flush=True)
-    if dist_on:
-        dist.barrier()
-        dist.destroy_process_group()
+    engine.barrier()
+    engine.close()
 
 
 if __name__ == "__main__":

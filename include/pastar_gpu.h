@@ -88,7 +88,10 @@ typedef struct pastar_node {
 
 /* Tuning of the device-resident search (all zero = defaults). */
 typedef struct pastar_search_opts {
-    int64_t batch_nodes;      /* target open nodes expanded per step        */
+    int64_t batch_nodes;      /* most open nodes expanded per step          */
+    int64_t batch_min;        /* a step with fewer nodes in its band also
+                                 takes the next bands (up to 4); 0 = 1/8 of
+                                 batch_nodes                               */
     int64_t table_slots_log2; /* open+closed hash table capacity (log2)     */
     int64_t pool_entries;     /* open-list entry pool (all f buckets)       */
     int64_t subqueue_entries; /* entries one bucket sub-queue can hold      */
@@ -96,7 +99,9 @@ typedef struct pastar_search_opts {
     int64_t band;             /* a step expands open nodes with f below the
                                  current minimum + band (0 = auto: half the
                                  mean f increase of one expansion)         */
-    int32_t profile;          /* 1: time the expand kernel with HIP events  */
+    int32_t profile;          /* 1: the expand kernel times each launch on
+                                 the 100 MHz device clock (s_memrealtime,
+                                 first block start -> last block end)      */
     int32_t verbose;
     int32_t no_autogrow;      /* 1: fail with PASTAR_ENOMEM instead of
                                  growing an exhausted capacity x4 and
@@ -118,7 +123,7 @@ typedef struct pastar_result {
     int64_t exchanged;      /* nodes sent to other shards                     */
     double seconds;         /* first expansion -> goal accepted (wall)        */
     double expand_ms;       /* sum of expand-kernel durations (profile = 1)   */
-    int64_t expand_launches;
+    int64_t expand_launches; /* launches with a batch (profile = 1) / steps   */
     int64_t expand_parents; /* parents handed to the expand kernel            */
     int64_t capacity_retries; /* restarts after growing an exhausted capacity */
     int64_t table_slots;    /* node table capacity used                       */
@@ -169,6 +174,12 @@ int pastar_group_create(int n_shards, pastar_group **out);
 void pastar_group_destroy(pastar_group *group); /* after its contexts */
 int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group *group, int shard_rank,
                               pastar_ctx **out);
+
+/* Element-wise reduction of count (<= 8) host int64 values over all shards
+ * (op 0 sum, 1 min, 2 max); collective.  Doubles as a barrier. */
+int pastar_gpu_allreduce(pastar_ctx *ctx, int64_t *vals, int count, int op);
+/* Wait for all work on the context's device. */
+int pastar_gpu_synchronize(pastar_ctx *ctx);
 
 /* Phase 1: PairAlign tables by the anti-diagonal wavefront kernel. */
 int pastar_gpu_build_heuristic(pastar_ctx *ctx);

@@ -43,6 +43,7 @@ class pastar_node(ctypes.Structure):
 class pastar_search_opts(ctypes.Structure):
     _fields_ = [
         ("batch_nodes", ctypes.c_int64),
+        ("batch_min", ctypes.c_int64),
         ("table_slots_log2", ctypes.c_int64),
         ("pool_entries", ctypes.c_int64),
         ("subqueue_entries", ctypes.c_int64),
@@ -101,6 +102,9 @@ SIGNATURES = {
     "pastar_group_destroy": (None, [ctypes.c_void_p]),
     "pastar_gpu_create_grouped": (ctypes.c_int, [ctypes.POINTER(pastar_problem), ctypes.c_int, ctypes.c_void_p,
                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "pastar_gpu_allreduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                            ctypes.c_int]),
+    "pastar_gpu_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "pastar_gpu_build_heuristic": (ctypes.c_int, [ctypes.c_void_p]),
     "pastar_gpu_pair_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]),
     "pastar_gpu_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void expand_api_kernel(const DevProblem *__
     const int group = lane / lpn, glane = lane % lpn;
     __shared__ int2 terms_all[kWaves][kTPerWave];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
-    const uint64_t gmask = (lpn == 64 ? ~0ull : ((1ull << lpn) - 1ull)) << (group * lpn);
+    const uint64_t gmask = (lpn == 64 ? ~0ull : ((1ull << (lpn & 63)) - 1ull)) << (group * lpn);
     const int per_block = kWaves * npw;
     for (int chunk = blockIdx.x; chunk * per_block < n_in; chunk += gridDim.x) {
         const int node = chunk * per_block + wave * npw + group;
@@ -217,6 +217,8 @@ constexpr int kBuckets = 2048;     // f buckets
 constexpr int kChunkLog2 = 12;     // entries per chunk = 4096 (32 KB)
 constexpr int kChunk = 1 << kChunkLog2;
 constexpr uint32_t kNoChunk = 0xffffffffu;
+constexpr int kWide = 4;                   // buckets a thin batch may span
+constexpr int kRanges = kWide * kSub;      // (bucket, sub-queue) ranges of a batch
 
 enum { kFailNear = 1, kFailFar = 2, kFailTable = 4, kFailOut = 8 };  // near = chunk pool, far = chunk table
 
@@ -231,7 +233,7 @@ struct Ctl {
     int band_log2;  // bucket width = 2^band_log2
     int f0;         // f of bucket 0 (h of the origin)
     int cur_b;      // lowest bucket that may hold entries (f_min only grows)
-    int batch_b;    // bucket of the current batch
+    int batch_b;    // first bucket of the current batch
     int n_shards;
     int fail_mask;  // kFail* bits of the capacity that ran out
     int has_work;   // select found a live bucket (multi-shard termination)
@@ -239,19 +241,31 @@ struct Ctl {
     unsigned long long pool_top, pool_chunks, maxch;
     unsigned long long table_slots;
     unsigned long long n_batch;
-    unsigned long long b_start[kSub], b_cnt[kSub], b_prefix[kSub + 1];
+    unsigned long long kmin;  // a batch smaller than this may pull the next buckets
+    unsigned long long b_start[kRanges], b_prefix[kRanges + 1];
     long long steps, max_steps;
     unsigned long long expanded, reopen, generated, claimed, dropped, parents;
+    // expand-kernel timing on the 100 MHz device clock (s_memrealtime): every
+    // block with work stamps its start and end into its own slot; select
+    // reduces them (first start -> last end) and sums over the launches
+    unsigned long long k_start, k_end, expand_ticks, timed_launches;
+    int timing;
+    int pad3;
 };
+
+__device__ __forceinline__ unsigned long long device_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 struct Queues {
     unsigned long long W[kBuckets][kSub];
     unsigned long long R[kBuckets][kSub];
 };
 
+constexpr int kMaxExpandBlocks = 4096;
+
 struct SearchArgs {
     const DevProblem *P;
     Ctl *ctl;
+    unsigned long long *stamps;  // [kMaxExpandBlocks][2] start / end, 0 = unused
     uint64_t *table;
     uint64_t cap_mask;
     Queues *q;
@@ -389,8 +403,35 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
     StepStats *st = a.stats;
     const int tid = threadIdx.x;
     __shared__ int found;
-    __shared__ unsigned long long avail[kSub];
+    __shared__ unsigned long long avail[kRanges], rstart[kRanges], take[kRanges];
+    __shared__ unsigned long long t_lo, t_hi;
+    if (ctl->timing) {
+        if (tid == 0) {
+            t_lo = ~0ull;
+            t_hi = 0;
+        }
+        __syncthreads();
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int k = tid; k < kMaxExpandBlocks; k += blockDim.x) {
+            const unsigned long long s0 = a.stamps[2 * k], s1 = a.stamps[2 * k + 1];
+            if (s0) {
+                lo = s0 < lo ? s0 : lo;
+                hi = s1 > hi ? s1 : hi;
+                a.stamps[2 * k] = 0;
+                a.stamps[2 * k + 1] = 0;
+            }
+        }
+        if (lo != ~0ull) {
+            atomicMin(&t_lo, lo);
+            atomicMax(&t_hi, hi);
+        }
+        __syncthreads();
+    }
     if (tid == 0) {
+        if (ctl->timing && ctl->n_batch && t_hi > t_lo) {
+            ctl->expand_ticks += t_hi - t_lo;
+            ctl->timed_launches++;
+        }
         ctl->expanded += st->expanded;
         ctl->reopen += st->reopen;
         ctl->generated += st->generated;
@@ -437,21 +478,36 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         }
         return;
     }
-    if (tid < kSub)
-        avail[tid] = a.q->W[b][tid] - a.q->R[b][tid];
+    // ranges r = (bucket b + r / kSub, sub-queue r % kSub); a thin batch
+    // (fewer than kmin entries) also takes the next buckets, up to kWide
+    if (tid < kRanges) {
+        const int bb = b + tid / kSub, sq = tid % kSub;
+        const bool in = bb <= limit && bb < kBuckets;
+        rstart[tid] = in ? a.q->R[bb][sq] : 0;
+        avail[tid] = in ? a.q->W[bb][sq] - rstart[tid] : 0;
+    }
     __syncthreads();
     if (tid == 0) {
         unsigned long long left = ctl->kmax, pre = 0;
-        for (int sq = 0; sq < kSub; sq++) {
-            const unsigned long long take = avail[sq] < left ? avail[sq] : left;
-            ctl->b_start[sq] = a.q->R[b][sq];
-            ctl->b_cnt[sq] = take;
-            ctl->b_prefix[sq] = pre;
-            a.q->R[b][sq] += take;
-            pre += take;
-            left -= take;
+        int r = 0;
+        for (int wb = 0; wb < kWide; wb++) {
+            if (wb > 0 && pre >= ctl->kmin)
+                break;
+            for (int sq = 0; sq < kSub; sq++, r++) {
+                const unsigned long long t = avail[r] < left ? avail[r] : left;
+                take[r] = t;
+                ctl->b_start[r] = rstart[r];
+                ctl->b_prefix[r] = pre;
+                pre += t;
+                left -= t;
+            }
         }
-        ctl->b_prefix[kSub] = pre;
+        for (; r < kRanges; r++) {
+            take[r] = 0;
+            ctl->b_start[r] = 0;
+            ctl->b_prefix[r] = pre;
+        }
+        ctl->b_prefix[kRanges] = pre;
         ctl->n_batch = pre;
         ctl->batch_b = b;
         ctl->cur_b = b;
@@ -460,19 +516,29 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         if (ctl->max_steps && ctl->steps >= ctl->max_steps)
             ctl->status = 3;
     }
+    __syncthreads();
+    if (tid < kRanges && take[tid])
+        a.q->R[b + tid / kSub][tid % kSub] = rstart[tid] + take[tid];
 }
 
-// Entry i of the current batch.
+// Entry i of the current batch (binary search over the range prefix in LDS).
 __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl, const unsigned long long *prefix,
                                              unsigned long long i)
 {
-    int sq = 0;
-    while (sq + 1 < kSub && prefix[sq + 1] <= i)
-        sq++;
-    const unsigned long long p = ctl->b_start[sq] + (i - prefix[sq]);
-    const uint32_t c = a.chunk_tab[((size_t)ctl->batch_b * kSub + sq) * ctl->maxch + (p >> kChunkLog2)];
+    int lo = 0, hi = kRanges - 1;  // last range with prefix[r] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (prefix[mid] <= i)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const int r = lo, bb = ctl->batch_b + r / kSub, sq = r % kSub;
+    const unsigned long long p = ctl->b_start[r] + (i - prefix[r]);
+    const uint32_t c = a.chunk_tab[((size_t)bb * kSub + sq) * ctl->maxch + (p >> kChunkLog2)];
     return a.pool[(size_t)(c - 1) * kChunk + (p & (kChunk - 1))];
 }
+
 
 // expand every entry of the batch (worker_inner's dequeue, closed check and
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
@@ -482,27 +548,29 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
     Ctl *ctl = a.ctl;
-    if (ctl->status)
-        return;
     const DevProblem &P = *a.P;
     const int n = N ? N : P.n;
-    const int npairs = P.npairs;
     const int lpn = (1 << n) < 64 ? (1 << n) : 64;
     const int npw = 64 / lpn;
+    const int per_block = kWaves * npw;
+    const unsigned long long nb = ctl->n_batch;
+    if (ctl->status || (unsigned long long)blockIdx.x * per_block >= nb)
+        return;  // blocks beyond the batch leave at once
+    const bool timing = ctl->timing;
+    const unsigned long long t_begin = timing ? device_clock() : 0;
+    const int npairs = P.npairs;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
     __shared__ int2 terms_all[kWaves][kTPerWave];
-    __shared__ unsigned long long prefix[kSub + 1];
+    __shared__ unsigned long long prefix[kRanges + 1];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
-    if (threadIdx.x <= kSub)
-        prefix[threadIdx.x] = ctl->b_prefix[threadIdx.x];
+    for (int r = threadIdx.x; r <= kRanges; r += blockDim.x)
+        prefix[r] = ctl->b_prefix[r];
     StepStats *st = a.stats;
     const int w = ctl->band_log2, f0 = ctl->f0;
-    const unsigned long long nb = ctl->n_batch;
     const int bound = *(volatile int *)a.goal_g;
     unsigned long long expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
-    const int per_block = kWaves * npw;
     const int masks = 1 << n;
     __syncthreads();
     for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
@@ -525,11 +593,15 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             const int h = (int)(s[KW + 1] >> 32);
             par_.g = (int)(best >> 32);
             par_.pmask = (int)(uint32_t)best;
+            // an entry is current iff its f is the node's f under the best g
+            // found so far; improvements are strict, so a current entry is
+            // unique and the closed mark needs no atomic
             ok = (par_.g + h == e.f) && e.f < bound;
             int verdict = ok ? 1 : 0;
             if (ok && glane == 0) {
-                const int old = atomicMin((int *)(a.table + (uint64_t)e.slot * SW + KW + 1), par_.g);
-                verdict = old <= par_.g ? 0 : (old != kIntMax ? 2 : 1);
+                int *closed = (int *)(a.table + (uint64_t)e.slot * SW + KW + 1);
+                verdict = *closed != kIntMax ? 2 : 1;
+                *closed = par_.g;
             }
             verdict = __shfl(verdict, leader_lane);
             ok = verdict != 0;
@@ -597,6 +669,14 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             atomicAdd(&st->ovf_table, ovf);
         if (stale)
             atomicAdd(&st->dropped, stale);
+    }
+    if (timing) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            a.stamps[2 * blockIdx.x] = t_begin;
+            a.stamps[2 * blockIdx.x + 1] = device_clock();
+        }
     }
 }
 

@@ -113,7 +113,7 @@ double now_s()
 // MPI ranks), LocalGroup for several shards driven by threads of one process
 // (peer copies; also how the sharded path is tested on a single GPU).
 // ---------------------------------------------------------------------------
-enum RedOp { kRedSum, kRedMin };
+enum RedOp { kRedSum, kRedMin, kRedMax };
 
 struct Transport {
     virtual ~Transport() = default;
@@ -194,7 +194,8 @@ class LocalTransport : public Transport {
         for (int k = 0; k < count; k++) {
             int64_t r = g_->vals[0][k];
             for (int s = 1; s < g_->G; s++)
-                r = op == kRedSum ? r + g_->vals[s][k] : std::min(r, g_->vals[s][k]);
+                r = op == kRedSum ? r + g_->vals[s][k]
+                                  : (op == kRedMin ? std::min(r, g_->vals[s][k]) : std::max(r, g_->vals[s][k]));
             vals[k] = r;
         }
         return sync();
@@ -257,6 +258,7 @@ struct pastar_ctx {
     DevBuf<Entry> pool;
     DevBuf<StepStats> stats;
     DevBuf<Ctl> ctl;
+    DevBuf<unsigned long long> stamps;
     DevBuf<int> goal;
     DevBuf<uint8_t> outbox, inbox;
     DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
@@ -272,6 +274,10 @@ struct pastar_ctx {
     int grown_log2 = 0;
     int last_fail_mask = 0;
     bool graph_used = false;
+    // per-problem search constants, computed once per context
+    bool origin_ready = false;
+    int32_t h0 = 0;
+    int auto_band_log2 = 0;
 };
 
 namespace {
@@ -736,7 +742,7 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
 namespace {
 
 struct SearchCfg {
-    unsigned long long kmax, pool_entries, subqueue_entries, outbox_cap;
+    unsigned long long kmax, kmin, pool_entries, subqueue_entries, outbox_cap;
     int table_log2;
     int verbose, profile, eager;
     int64_t max_steps;
@@ -763,6 +769,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         PA_TRY(c->pool.alloc((size_t)chunks * kChunk));
         PA_TRY(c->stats.alloc(1));
         PA_TRY(c->ctl.alloc(1));
+        PA_TRY(c->stamps.alloc(2 * kMaxExpandBlocks));
         PA_TRY(c->goal.alloc(1));
         if (c->n_shards > 1) {
             const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
@@ -785,6 +792,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
     HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
+    HIP_TRY(hipMemsetAsync(c->stamps.p, 0, sizeof(unsigned long long) * 2 * kMaxExpandBlocks, c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
     return PASTAR_OK;
 }
@@ -834,10 +842,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     const int per_block = kWaves * (64 / lpn);
     const size_t rb = remote_bytes(KW);
 
-    // h of the origin and the bucket width
+    // h of the origin and the bucket width (once per context)
     uint16_t zero[PASTAR_MAX_SEQ] = {0};
-    int32_t h0 = 0;
-    {
+    if (!c->origin_ready) {
         DevBuf<uint16_t> dpos;
         DevBuf<int32_t> dh;
         PA_TRY(dpos.alloc(PASTAR_MAX_SEQ));
@@ -846,25 +853,33 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hipLaunchKernelGGL(h_kernel, dim3(1), dim3(64), 0, c->stream, c->dP.p, dpos.p, 1, dh.p);
         PA_TRY(check_launch());
         HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(hipMemcpy(&h0, dh.p, 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&c->h0, dh.p, 4, hipMemcpyDeviceToHost));
+        PA_TRY(estimate_band_log2(c, c->h0, 0, &c->auto_band_log2));
+        c->origin_ready = true;
     }
-    int w = 0;
-    PA_TRY(estimate_band_log2(c, h0, cfg.band, &w));
+    const int32_t h0 = c->h0;
+    int w = c->auto_band_log2;
+    if (cfg.band > 0)
+        PA_TRY(estimate_band_log2(c, h0, cfg.band, &w));
 
     Ctl hc{};
     hc.band_log2 = w;
     hc.f0 = h0;
     hc.n_shards = G;
     hc.kmax = cfg.kmax;
+    hc.kmin = cfg.kmin;
     hc.pool_chunks = pool_chunks_of(cfg);
     hc.maxch = maxch_of(cfg);
     hc.table_slots = c->nslots;
     hc.max_steps = cfg.max_steps;
+    hc.k_start = ~0ull;
+    hc.timing = cfg.profile ? 1 : 0;
     HIP_TRY(hipMemcpy(c->ctl.p, &hc, sizeof(Ctl), hipMemcpyHostToDevice));
 
     SearchArgs a{};
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
+    a.stamps = c->stamps.p;
     a.table = c->table.p;
     a.cap_mask = c->nslots - 1;
     a.q = c->queues.p;
@@ -876,7 +891,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.outbox_cap = cfg.outbox_cap;
 
     const dim3 blk(kBlock);
-    const dim3 expand_grid((unsigned)std::min<unsigned long long>(4096, (cfg.kmax + per_block - 1) / per_block));
+    const dim3 expand_grid(
+        (unsigned)std::min<unsigned long long>(kMaxExpandBlocks, (cfg.kmax + per_block - 1) / per_block));
 
     // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
     // its owner shard, through the same relax path as remote records
@@ -904,32 +920,15 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     const double t0 = now_s();
     if (G == 1) {
         // runs of S steps captured once, replayed until `select` reports
-        // termination (event nodes around each expand when profiling)
+        // termination; with profiling the expand kernel times itself on the
+        // device clock (event nodes inside a graph cost several microseconds
+        // per step)
         const int S = 32;
-        std::vector<hipEvent_t> evs;
-        if (cfg.profile) {
-            evs.resize(2 * S);
-            for (auto &e : evs)
-                HIP_TRY(hipEventCreate(&e));
-        }
         c->graph_used = false;
-        auto enqueue_steps = [&](bool capturing) -> hipError_t {
+        auto enqueue_steps = [&](bool) -> hipError_t {
             for (int k = 0; k < S; k++) {
                 hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
-                if (cfg.profile) {
-                    hipError_t e = capturing ? hipEventRecordWithFlags(evs[2 * k], c->stream, hipEventRecordExternal)
-                                             : hipEventRecord(evs[2 * k], c->stream);
-                    if (e != hipSuccess)
-                        return e;
-                }
                 ops.expand(expand_grid, blk, c->stream, a);
-                if (cfg.profile) {
-                    hipError_t e = capturing
-                                       ? hipEventRecordWithFlags(evs[2 * k + 1], c->stream, hipEventRecordExternal)
-                                       : hipEventRecord(evs[2 * k + 1], c->stream);
-                    if (e != hipSuccess)
-                        return e;
-                }
             }
             return hipGetLastError();
         };
@@ -970,13 +969,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             }
             h = *c->h_ctl;
             const long long ran = h.steps - steps_before;
-            if (cfg.profile) {
-                for (long long k = 0; k < ran && k < S; k++) {
-                    float ms = 0;
-                    if (hipEventElapsedTime(&ms, evs[2 * k], evs[2 * k + 1]) == hipSuccess)
-                        expand_ms += ms;
-                }
-            }
             launches += ran;
             steps_before = h.steps;
             if (h.status)
@@ -990,27 +982,16 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             (void)hipGraphExecDestroy(exec);
         if (graph)
             (void)hipGraphDestroy(graph);
-        for (auto &e : evs)
-            (void)hipEventDestroy(e);
         PA_TRY(rc);
     } else {
         for (;;) {
             hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
-            if (cfg.profile)
-                HIP_TRY(hipEventRecord(c->ev0, c->stream));
             ops.expand(expand_grid, blk, c->stream, a);
-            if (cfg.profile)
-                HIP_TRY(hipEventRecord(c->ev1, c->stream));
             PA_TRY(check_launch());
             // exchange: counts, then the records (grouped point-to-point over xGMI)
             HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
-            if (cfg.profile) {
-                float ms = 0;
-                HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-                expand_ms += ms;
-            }
             launches++;
             const int had_work = c->h_ctl->has_work;
             std::vector<unsigned long long> send(G), recv(G);
@@ -1100,6 +1081,25 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     res->steps = h.steps;
     res->exchanged = exchanged;
     res->seconds = t1 - t0;
+    {
+        unsigned long long ticks = h.expand_ticks, timed = h.timed_launches;
+        if (h.timing && h.n_batch) {  // the last launch, not yet reduced by a select
+            std::vector<unsigned long long> st(2 * kMaxExpandBlocks);
+            HIP_TRY(hipMemcpy(st.data(), c->stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long lo = ~0ull, hi = 0;
+            for (int k = 0; k < kMaxExpandBlocks; k++)
+                if (st[2 * k]) {
+                    lo = std::min(lo, st[2 * k]);
+                    hi = std::max(hi, st[2 * k + 1]);
+                }
+            if (hi > lo) {
+                ticks += hi - lo;
+                timed++;
+            }
+        }
+        expand_ms = (double)ticks * 1e-5;  // 100 MHz device clock
+        launches = h.timing ? (int64_t)timed : (int64_t)h.steps;
+    }
     res->expand_ms = expand_ms;
     res->expand_launches = launches;
     res->expand_parents = (int64_t)h.parents;
@@ -1130,6 +1130,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     SearchCfg cfg;
     const unsigned long long masks = (1ull << c->n) - 1;
     cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 32768ull;
+    cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 22;
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
@@ -1320,7 +1321,8 @@ int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
     DevBuf<int64_t> d;
     PA_TRY(d.alloc((size_t)count));
     HIP_TRY(hipMemcpyAsync(d.p, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
-    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, op == kRedSum ? ncclSum : ncclMin, comm_, c->stream));
+    const ncclRedOp_t nop = op == kRedSum ? ncclSum : (op == kRedMin ? ncclMin : ncclMax);
+    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, nop, comm_, c->stream));
     HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return PASTAR_OK;
@@ -1441,6 +1443,29 @@ int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group 
         }
         (void)hipGetLastError();
     }
+    return PASTAR_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int pastar_gpu_allreduce(pastar_ctx *c, int64_t *vals, int count, int op)
+{
+    if (!c || !vals || count < 0 || count > 8 || op < 0 || op > 2)
+        return fail(PASTAR_EINVAL, "invalid allreduce arguments");
+    if (!c->tr || c->n_shards == 1)
+        return PASTAR_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    return c->tr->allreduce(c, vals, count, (RedOp)op);
+}
+
+int pastar_gpu_synchronize(pastar_ctx *c)
+{
+    if (!c)
+        return fail(PASTAR_EINVAL, "null ctx");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
     return PASTAR_OK;
 }
 

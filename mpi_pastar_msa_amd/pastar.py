@@ -117,6 +117,7 @@ class PAStarOpt:
     hash_shift: int = 12
     threads_num: int = 1
     batch_nodes: int = 0
+    batch_min: int = 0
     table_slots_log2: int = 0
     pool_entries: int = 0
     subqueue_entries: int = 0
@@ -128,7 +129,7 @@ class PAStarOpt:
     eager: bool = False
 
     def search_opts(self):
-        return nat.pastar_search_opts(self.batch_nodes, self.table_slots_log2, self.pool_entries,
+        return nat.pastar_search_opts(self.batch_nodes, self.batch_min, self.table_slots_log2, self.pool_entries,
                                       self.subqueue_entries, self.max_steps, self.band, int(self.profile),
                                       int(self.verbose),
                                       int(not self.autogrow), int(self.eager))
@@ -242,6 +243,19 @@ class Engine:
 
     def __exit__(self, *a):
         self.close()
+
+    # ---- collectives over the shards ----
+    def allreduce(self, values, op="sum"):
+        """Element-wise sum/min/max of up to 8 integers over all shards."""
+        arr = (ctypes.c_int64 * len(values))(*[int(v) for v in values])
+        check(lib().pastar_gpu_allreduce(self._ctx, arr, len(values), {"sum": 0, "min": 1, "max": 2}[op]))
+        return list(arr)
+
+    def barrier(self):
+        self.allreduce([0])
+
+    def synchronize(self):
+        check(lib().pastar_gpu_synchronize(self._ctx))
 
     # ---- HeuristicHPair ----
     def init(self):

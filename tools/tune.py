@@ -17,7 +17,8 @@ from mpi_pastar_msa_amd import Engine, PAStarOpt, Sequences  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("workload")
 ap.add_argument("--mult", default="0.125,0.25,0.5,1,2")
-ap.add_argument("--batch", default="8192")
+ap.add_argument("--batch", default="32768")
+ap.add_argument("--kmin", type=int, default=0)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--table-log2", type=int, default=0)
 a = ap.parse_args()
@@ -33,7 +34,7 @@ for b in [int(x) for x in a.batch.split(",")]:
         best = None
         for _ in range(a.reps):
             t0 = time.perf_counter()
-            r = e.pa_star(PAStarOpt(batch_nodes=b, band=band, table_slots_log2=a.table_log2))
+            r = e.pa_star(PAStarOpt(batch_nodes=b, batch_min=a.kmin, band=band, table_slots_log2=a.table_log2))
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         print("batch %6d band %7d (x%.3f): score %d exp %9d reopen %8d steps %6d wall %.4f s  call %.4f s  %.3g exp/s"
