@@ -1,0 +1,268 @@
+"""world_size-2 (and 3) CPU tests of the sharded path over torch.distributed
+`gloo`.  No GPU.
+
+The device search shards one A* by the reference's owner hash
+(CoordHash.cpp / Sequences::get_id, z-order by default): every node lives on
+exactly one shard, children are routed to their owner, and each step ends in
+an exchange (counts, then records), a MIN allreduce of the goal g and a SUM
+allreduce of the has-work flags (pastar_gpu.hip, search_impl, G > 1 branch).
+`ShardModel` below restates that protocol step for step on the CPU, with the
+oracle's Node::getNeigh as the expansion and gloo as the transport, so the
+protocol itself (termination rule, goal bound, reopening, owner routing,
+backtrace across owners) is exercised with several ranks here; the HIP
+implementation of the same protocol is covered on one GPU with 2-8 shards in
+tests/test_gpu_parity.py (sharded search), and RCCL across GPUs by the
+driver's multi-GPU bench.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_bind as orc
+from conftest import ROOT, golden
+
+INT_MAX = 2**31 - 1
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(world, fn, *args):
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, val = q.get(timeout=240)
+        out[rank] = val
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        if isinstance(out[r], BaseException):
+            raise out[r]
+    return [out[r] for r in range(world)]
+
+
+def _entry(rank, world, port, fn, args, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, ROOT)
+    try:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+        val = fn(rank, world, *args)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # report to the parent instead of hanging it
+        val = RuntimeError("rank %d: %r" % (rank, e))
+    q.put((rank, val))
+
+
+class ShardModel:
+    """One shard of the sharded search (search_impl, G > 1): a node table
+    (pos -> best g, parent mask, closed), f-bucketed open lists of width
+    2**band_log2 above f0 = h(origin), an outbox per destination shard."""
+
+    def __init__(self, o, rank, world, band_log2, batch):
+        self.o, self.rank, self.world = o, rank, world
+        self.band, self.batch = band_log2, batch
+        self.best = {}      # pos -> (g, parenti)
+        self.closed = {}    # pos -> g it was expanded with
+        self.buckets = {}   # bucket -> [(pos, g, f, parenti)]
+        self.goal_pos = tuple(o.lengths)
+        self.goal_g = INT_MAX
+        self.f0 = o.initial_node()[2]
+        self.expanded = 0
+        self.sent = 0
+
+    def bucket(self, f):
+        return max(0, (f - self.f0) >> self.band)
+
+    def relax(self, node):
+        """relax() in device.hpp: improved iff strictly lower g."""
+        pos, g, f, par = node
+        b = self.best.get(pos)
+        if b is not None and b[0] <= g:
+            return
+        self.best[pos] = (g, par)
+        if pos == self.goal_pos:
+            self.goal_g = min(self.goal_g, g)
+            return
+        self.buckets.setdefault(self.bucket(f), []).append(node)
+
+    def step(self):
+        """select_kernel + expand_kernel: the lowest live bucket not above the
+        goal's, at most `batch` entries; stale entries (g no longer the
+        best) are dropped.  Returns (had_work, outboxes)."""
+        outbox = [[] for _ in range(self.world)]
+        limit = self.bucket(self.goal_g) if self.goal_g < INT_MAX else None
+        live = sorted(b for b, v in self.buckets.items() if v and (limit is None or b <= limit))
+        if not live:
+            return 0, outbox
+        b = live[0]
+        batch, self.buckets[b] = self.buckets[b][:self.batch], self.buckets[b][self.batch:]
+        for node in batch:
+            pos, g = node[0], node[1]
+            if self.best[pos][0] != g:
+                continue  # stale
+            if self.goal_g < INT_MAX and node[2] >= self.goal_g:
+                continue  # goal bound
+            self.closed[pos] = g
+            self.expanded += 1
+            for kid, owner in self.o.get_neigh(node, self.world, 0, 12):
+                outbox[owner].append(kid)
+        return 1, outbox
+
+    def exchange(self, outbox):
+        """exchange_counts + exchange_records (the RCCL grouped send/recv)."""
+        n = self.o.n
+        width = n + 3
+        counts = torch.tensor([len(v) for v in outbox], dtype=torch.int64)
+        all_counts = [torch.zeros(self.world, dtype=torch.int64) for _ in range(self.world)]
+        dist.all_gather(all_counts, counts)
+        reqs, inbox = [], []
+        for d in range(self.world):
+            if d == self.rank:
+                continue
+            if outbox[d]:
+                t = torch.tensor([list(k[0]) + [k[1], k[2], k[3]] for k in outbox[d]], dtype=torch.int64)
+                reqs.append(dist.isend(t, d))
+                self.sent += len(outbox[d])
+            m = int(all_counts[d][self.rank])
+            if m:
+                t = torch.zeros((m, width), dtype=torch.int64)
+                reqs.append(dist.irecv(t, d))
+                inbox.append(t)
+        for r in reqs:
+            r.wait()
+        recs = list(outbox[self.rank])
+        for t in inbox:
+            recs += [(tuple(row[:n]), row[n], row[n + 1], row[n + 2]) for row in t.tolist()]
+        return recs
+
+    def search(self):
+        origin = self.o.initial_node()
+        if orc.get_id(list(origin[0]), self.world, 0, 12) == self.rank:
+            self.relax(origin)
+        steps = 0
+        while True:
+            had, outbox = self.step()
+            for rec in self.exchange(outbox):
+                self.relax(rec)
+            t = torch.tensor([self.goal_g], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            self.goal_g = int(t)
+            h = torch.tensor([had], dtype=torch.int64)
+            dist.all_reduce(h)
+            steps += 1
+            if int(h) == 0:
+                return steps
+
+    def walk(self):
+        """walk_kernel + broadcast: the owner of the current node names its
+        parent, until the origin."""
+        n = self.o.n
+        pos, path = self.goal_pos, [self.goal_pos]
+        while any(pos):
+            owner = orc.get_id(list(pos), self.world, 0, 12)
+            t = torch.zeros(1, dtype=torch.int64)
+            if owner == self.rank:
+                t[0] = self.best[pos][1]
+            dist.broadcast(t, owner)
+            mask = int(t)
+            pos = tuple(pos[d] - ((mask >> d) & 1) for d in range(n))
+            path.append(pos)
+        return path[::-1]
+
+
+def rows_from_path(seqs, path):
+    rows = ["" for _ in seqs]
+    for a, b in zip(path, path[1:]):
+        for d, s in enumerate(seqs):
+            rows[d] += s[a[d]] if b[d] > a[d] else "-"
+    return rows
+
+
+def _sharded_search(rank, world, fasta, band_log2, batch):
+    o = orc.Oracle(fasta=fasta)
+    m = ShardModel(o, rank, world, band_log2, batch)
+    steps = m.search()
+    goal_owner = orc.get_id(list(m.goal_pos), world, 0, 12)
+    path = m.walk()
+    rows = rows_from_path(o.seqs, path)
+    # every node has exactly one owner: nothing this shard holds belongs elsewhere
+    foreign = sum(1 for p in m.best if orc.get_id(list(p), world, 0, 12) != rank)
+    return {"goal_g": m.goal_g, "steps": steps, "expanded": m.expanded, "sent": m.sent,
+            "rows": rows, "cost": o.alignment_cost(rows), "foreign": foreign,
+            "goal_owner_has_goal": (rank != goal_owner) or (m.goal_pos in m.best),
+            "nodes": len(m.best)}
+
+
+CASES = [("test2", 2, 4, 64), ("PF08184", 2, 6, 16), ("test", 2, 0, 1 << 20),
+         ("test2", 3, 8, 8), ("syn4x200_s1", 2, 13, 4096)]
+
+
+@pytest.mark.parametrize("name,world,band_log2,batch", CASES)
+def test_sharded_protocol_reaches_reference_optimum(name, world, band_log2, batch, kat):
+    ref = kat["inputs"][name]
+    res = run_ranks(world, _sharded_search, golden(ref["file"]), band_log2, batch)
+    for r in res:
+        assert r["goal_g"] == ref["score"]
+        assert r["cost"] == ref["score"]
+        assert r["foreign"] == 0
+        assert r["goal_owner_has_goal"]
+        assert r["rows"] == res[0]["rows"]
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    assert [row.replace("-", "") for row in res[0]["rows"]] == o.seqs
+    assert sum(r["sent"] for r in res) > 0  # the exchange really carried nodes
+    assert all(r["expanded"] > 0 for r in res) or ref["expansions_t1"] < 30
+
+
+def _owners_cover(rank, world, fasta):
+    """Every child of every expansion is routed to exactly one shard in
+    [0, world), and the union of what the shards receive is the whole set."""
+    o = orc.Oracle(fasta=fasta)
+    node = o.initial_node()
+    frontier, seen = [node], []
+    for _ in range(6):
+        nxt = []
+        for nd in frontier:
+            for kid, owner in o.get_neigh(nd, world, 0, 12):
+                assert 0 <= owner < world
+                assert owner == orc.get_id(list(kid[0]), world, 0, 12)
+                seen.append((kid[0], owner))
+                nxt.append(kid)
+        frontier = nxt[:50]
+    mine = sorted({p for p, w in seen if w == rank})
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine)
+    allpos = sorted({p for p, _ in seen})
+    return sorted(p for g in gathered for p in g) == allpos
+
+
+def test_owner_partition_covers_every_node():
+    assert all(run_ranks(2, _owners_cover, golden("test2.fasta")))
+
+
+def _share_id(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import bench
+    rid = bench.share_rccl_id(rank, world, lambda: bytes(range(128)))
+    return rid
+
+
+def test_bench_rccl_id_rendezvous():
+    port = free_port() - 17
+    res = run_ranks(2, _share_id, port)
+    assert res[0] == res[1] == bytes(range(128))

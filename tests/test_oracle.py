@@ -1,0 +1,137 @@
+"""CPU tests of the oracle itself: pinned against the reference's known-answer
+values (tests/golden/kat.json), the reference's own Cost.cpp + PairAlign.cpp
+(oracle/_ref, built where /root/reference exists) and the extracted distance
+table (tests/golden/cost_table.json).  No GPU."""
+import hashlib
+import json
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_bind as orc
+from conftest import GOLDEN, golden
+
+REF_PAIRALIGN = os.path.join(orc.ORACLE_DIR, "_ref", "ref_pairalign")
+SMALL = ["test", "test2", "PF08184", "syn4x200_s1"]
+
+
+def md5_rows(rows):
+    return hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest()
+
+
+def test_synthetic_fixtures_match_generator(kat):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "tools"))
+    import gen_synthetic
+    for name, md5 in kat["fasta_md5"].items():
+        text = gen_synthetic.preset_fasta(name.replace(".fasta", ""))
+        assert hashlib.md5(text.encode()).hexdigest() == md5
+        with open(golden(name)) as f:
+            assert f.read() == text
+
+
+def test_cost_table_matches_extracted_fixture():
+    with open(golden("cost_table.json")) as f:
+        cells = json.load(f)["cells"]
+    for r in range(128):
+        for l in range(128):
+            key = chr(r) + chr(l)
+            want = cells.get(key, 0) if r < 90 and l < 90 else 0
+            assert orc.cost(r, l) == want, key
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PAIRALIGN), reason="reference slice not built (no /root/reference)")
+def test_cost_table_matches_reference_binary():
+    out = subprocess.check_output([REF_PAIRALIGN, "--cost"], text=True).split("\n")
+    for r in range(90):
+        row = [int(v) for v in out[r].split()]
+        assert row == [orc.cost(r, l) for l in range(90)]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PAIRALIGN), reason="reference slice not built (no /root/reference)")
+def test_pairalign_matches_reference_binary(kat):
+    rng = random.Random(3)
+    cases = []
+    for name in ["test", "test2", "PF08184", "kinase"]:
+        o = orc.Oracle(fasta=golden(kat["inputs"][name]["file"]))
+        cases += [(o.seqs[x], o.seqs[y]) for x, y in o.pairs[:3]]
+    # codes >= 90 ('Z' and up) index past the reference's 90x90 table (Cost.cpp,
+    # undefined behaviour there; the oracle and the product define them as 0)
+    alphabet = "ACDEFGHIKLMNPQRSTVWYBX-"
+    for _ in range(12):
+        cases.append(("".join(rng.choice(alphabet) for _ in range(rng.randint(1, 40))),
+                      "".join(rng.choice(alphabet) for _ in range(rng.randint(1, 40)))))
+    for s1, s2 in cases:
+        out = subprocess.check_output([REF_PAIRALIGN, s1, s2], text=True).split("\n")
+        l1, l2 = map(int, out[0].split())
+        ref = np.array([[int(v) for v in out[1 + i].split()] for i in range(l1 + 1)], dtype=np.int32)
+        np.testing.assert_array_equal(orc.pairalign(s1, s2), ref)
+
+
+@pytest.mark.parametrize("name", SMALL + ["kinase"])
+def test_known_answers_heuristic_and_first_expansion(name, kat):
+    ref = kat["inputs"][name]
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    if "weights" in ref:
+        assert o.weights == ref["weights"]
+    node = o.initial_node()
+    assert node[2] == ref["h_origin"]
+    kids = [k for k, _ in o.get_neigh(node)]
+    fe = ref["first_expansion"]
+    assert len(kids) == fe["count"]
+    assert sum(k[1] for k in kids) == fe["sum_g"]
+    assert sum(k[2] - k[1] for k in kids) == fe["sum_h"]
+    assert [kids[0][1], kids[0][2] - kids[0][1]] == fe["first"]
+    assert [kids[-1][1], kids[-1][2] - kids[-1][1]] == fe["last"]
+
+
+def test_zorder_owner_kat(kat):
+    z = kat["zorder_kat"]
+    for n, owners in z["owners"].items():
+        c = [(7 * (i + 1)) % 13 for i in range(int(n))]
+        assert [orc.get_id(c, s, 0, 12) for s in z["sizes"]] == owners
+
+
+@pytest.mark.parametrize("name", SMALL + ["syn8x400_s11"])
+def test_serial_search_matches_reference(name, kat):
+    """Score, `-t 1` expansion count (Boost.MultiIndex tie order), similarity and
+    alignment of the reference's serial search."""
+    ref = kat["inputs"][name]
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    r = o.astar()
+    assert r["score"] == ref["score"]
+    assert r["expansions"] == ref["expansions_t1"]
+    if "similarity" in ref:
+        assert "%.2f" % r["similarity"] == ref["similarity"]
+    if "alignment_md5" in ref:
+        assert md5_rows(r["rows"]) == ref["alignment_md5"]
+    assert o.alignment_cost(r["rows"]) == ref["score"]
+    assert [row.replace("-", "") for row in r["rows"]] == o.seqs
+
+
+@pytest.mark.slow
+def test_serial_search_kinase(kat):
+    """kinase at -t 1: 4 497 279 expansions, score 421546 (about 40 s)."""
+    ref = kat["inputs"]["kinase"]
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    r = o.astar()
+    assert (r["score"], r["expansions"]) == (ref["score"], ref["expansions_t1"])
+    assert md5_rows(r["rows"]) == ref["alignment_md5"]
+
+
+def test_fasta_reader_quirks(tmp_path):
+    """read_fasta.cpp:21-34: a blank line ends a sequence (so a blank line inside
+    a record starts a new one), '\\r' is kept, headers are dropped."""
+    p = tmp_path / "q.fasta"
+    p.write_bytes(b">a\nACD\nEF\n\nGH\n>b\r\nKLM\r\n>c\nNP")
+    o = orc.Oracle(fasta=p)
+    assert o.seqs == ["ACDEF", "GH", "KLM\r", "NP"]
+
+
+def test_alignment_cost_rejects_invalid(kat):
+    o = orc.Oracle(fasta=golden("test2.fasta"))
+    rows = o.astar()["rows"]
+    assert o.alignment_cost([r[:-1] for r in rows]) == -1  # does not reach the goal
