@@ -12,7 +12,7 @@
  *   HeuristicHPair::calculate_h (:74-86)           pastar_gpu_h
  *   PairAlign::getScore (PairAlign.cpp:174-177)    pastar_gpu_pair_table
  *   Node<N>::getNeigh (Node.cpp:206-248, Node.h:37) pastar_gpu_expand
- *   Coord<N>::get_id (CoordHash.cpp:191-245)       pastar_gpu_owner
+ *   Coord<N>::get_id (CoordHash.cpp:191-245)       pastar_owner
  *   PAStar<N>::pa_star (PAStar.cpp:627-673,        pastar_gpu_search
  *     PAStar.h:117) incl. worker_inner,
  *     OpenList / ClosedList (PriorityList.h:52-82,
