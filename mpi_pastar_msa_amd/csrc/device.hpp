@@ -52,22 +52,28 @@ struct Entry {  // open-pile entry
     int32_t f;
 };
 
-// Per-step counters (two sets, alternating with the step parity).
+// Per-step counters.  The counters every wave adds to are spread over
+// kStatRows rows (row = global wave index % kStatRows): a single word takes
+// one atomic per wave and saturates at ~88 atomics/us, which at 5-10 K waves
+// per step would serialise for 50-100 us; select sums the rows.
+constexpr int kStatRows = 64;
+enum { kStExpanded, kStReopen, kStGenerated, kStClaimed, kStDropped, kStOvfTable, kStFields = 8 };
 struct StepStats {
-    unsigned long long pad0[3];
-    unsigned long long expanded;      // parents that passed stale/closed checks
-    unsigned long long reopen;
-    unsigned long long generated;     // border-valid children
-    unsigned long long claimed;       // new table slots
-    unsigned long long outbox_total;
-    unsigned long long ovf_near;      // chunk pool exhausted
-    unsigned long long ovf_far;       // sub-queue chunk table exhausted
-    unsigned long long ovf_table;     // node table probe limit hit
-    unsigned long long ovf_out;       // outbox capacity exceeded
-    unsigned long long dropped;       // pruned by f >= bound / stale
-    unsigned long long pad[3];
+    // expanded: parents that passed the stale/closed checks; reopen; generated:
+    // border-valid children; claimed: new table slots; dropped: stale or
+    // pruned parents; ovf_table: node table probe limit hit
+    unsigned long long row[kStatRows][kStFields];
+    unsigned long long ovf_near;  // chunk pool exhausted
+    unsigned long long ovf_far;   // sub-queue chunk table exhausted
+    unsigned long long ovf_out;   // outbox capacity exceeded
+    unsigned long long pad;
     unsigned long long outbox_count[8];
 };
+
+__device__ __forceinline__ unsigned long long *stat_row(StepStats *st, unsigned wave_global)
+{
+    return st->row[wave_global % kStatRows];
+}
 
 // Remote record sent to the owner shard over RCCL.
 template <int KW>

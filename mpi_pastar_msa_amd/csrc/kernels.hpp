@@ -219,13 +219,14 @@ constexpr int kChunk = 1 << kChunkLog2;
 constexpr uint32_t kNoChunk = 0xffffffffu;
 constexpr int kWide = 4;                   // buckets a thin batch may span
 constexpr int kRanges = kWide * kSub;      // (bucket, sub-queue) ranges of a batch
+constexpr int kArrive = 64;                // first-level arrival counters of expand
 
 enum { kFailNear = 1, kFailFar = 2, kFailTable = 4, kFailOut = 8 };  // near = chunk pool, far = chunk table
 
-__host__ __device__ inline int fail_bits(const StepStats &s)
+__host__ __device__ inline int fail_bits(unsigned long long near, unsigned long long far, unsigned long long table,
+                                          unsigned long long out)
 {
-    return (s.ovf_near ? kFailNear : 0) | (s.ovf_far ? kFailFar : 0) | (s.ovf_table ? kFailTable : 0) |
-           (s.ovf_out ? kFailOut : 0);
+    return (near ? kFailNear : 0) | (far ? kFailFar : 0) | (table ? kFailTable : 0) | (out ? kFailOut : 0);
 }
 
 struct Ctl {
@@ -245,12 +246,17 @@ struct Ctl {
     unsigned long long b_start[kRanges], b_prefix[kRanges + 1];
     long long steps, max_steps;
     unsigned long long expanded, reopen, generated, claimed, dropped, parents;
-    // expand-kernel timing on the 100 MHz device clock (s_memrealtime): every
-    // block with work stamps its start and end into its own slot; select
-    // reduces them (first start -> last end) and sums over the launches
+    // expand-kernel timing on the 100 MHz device clock (s_memrealtime): the
+    // first kArrive blocks stamp their start (blocks are dispatched in index
+    // order), the last block to finish takes the earliest stamp and its own
+    // end, and sums over the launches
     unsigned long long k_start, k_end, expand_ticks, timed_launches;
     int timing;
-    int pad3;
+    int fuse;  // 1: the last expand block also runs select for the next step
+    // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
+    // then the groups), reset by the last block
+    unsigned arrive_top;
+    unsigned arrive[kArrive];
 };
 
 __device__ __forceinline__ unsigned long long device_clock() { return __builtin_amdgcn_s_memrealtime(); }
@@ -265,7 +271,7 @@ constexpr int kMaxExpandBlocks = 4096;
 struct SearchArgs {
     const DevProblem *P;
     Ctl *ctl;
-    unsigned long long *stamps;  // [kMaxExpandBlocks][2] start / end, 0 = unused
+    unsigned long long *stamps;  // [kArrive] start stamps of the first blocks
     uint64_t *table;
     uint64_t cap_mask;
     Queues *q;
@@ -294,7 +300,9 @@ __device__ __forceinline__ int bucket_of(int f, int f0, int w)
 // Write entry e at position p of sub-queue (b, sq).  The lane whose position
 // opens a chunk allocates it; the others wait for its publication (the
 // allocating wave reserved an earlier range, so it is resident and past its
-// reservation).
+// reservation).  The chunk id is the only datum handed over, so the
+// publication is relaxed (an agent-scope release or acquire would write back
+// or invalidate the L2 on every append).
 __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, unsigned long long p, const Entry &e,
                                             StepStats *st)
 {
@@ -309,10 +317,10 @@ __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, 
     if (off == 0) {
         const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
         const uint32_t v = id < a.ctl->pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
-        __hip_atomic_store(tp, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(tp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint32_t c;
-    while ((c = __hip_atomic_load(tp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+    while ((c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
         __builtin_amdgcn_s_sleep(1);
     if (c == kNoChunk) {
         atomicAdd(&st->ovf_near, 1ull);
@@ -391,54 +399,62 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
     }
 }
 
+// Loads of words other blocks of the same launch update with atomics (the
+// fused select runs in the last expand block): coherent across XCDs.
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // select: account the previous step, then cut the next batch from the lowest
 // bucket holding entries below the best goal (PAStar::check_stop's
 // termination, PAStar.cpp:480-547: the goal is accepted once no open node has
-// f below its g).  One block of kBlock threads.
-__global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
+// f below its g).  Run by one whole block of kBlock threads: as its own
+// launch (sharded search, where the exchange sits between expand and
+// select) or as the tail of the last expand block (one shard).
+__device__ __forceinline__ void select_block(const SearchArgs &a)
 {
     Ctl *ctl = a.ctl;
     if (ctl->status)
         return;
     StepStats *st = a.stats;
     const int tid = threadIdx.x;
-    __shared__ int found;
+    static_assert(kStatRows == 64, "one wave sums the stat rows");
+    __shared__ int found, goal_s, cur_s;
     __shared__ unsigned long long avail[kRanges], rstart[kRanges], take[kRanges];
-    __shared__ unsigned long long t_lo, t_hi;
-    if (ctl->timing) {
+    __shared__ unsigned long long sums[kStFields], ovf[3];
+    // one round trip: every word select needs from the finished step
+    if (tid < kStatRows) {
+        unsigned long long v[kStFields];
+#pragma unroll
+        for (int f = 0; f < kStFields; f++)
+            v[f] = ld_agent(&st->row[tid][f]);
+#pragma unroll
+        for (int f = 0; f < kStFields; f++)
+            v[f] = wave_sum(v[f]);
         if (tid == 0) {
-            t_lo = ~0ull;
-            t_hi = 0;
+#pragma unroll
+            for (int f = 0; f < kStFields; f++)
+                sums[f] = v[f];
         }
-        __syncthreads();
-        unsigned long long lo = ~0ull, hi = 0;
-        for (int k = tid; k < kMaxExpandBlocks; k += blockDim.x) {
-            const unsigned long long s0 = a.stamps[2 * k], s1 = a.stamps[2 * k + 1];
-            if (s0) {
-                lo = s0 < lo ? s0 : lo;
-                hi = s1 > hi ? s1 : hi;
-                a.stamps[2 * k] = 0;
-                a.stamps[2 * k + 1] = 0;
-            }
-        }
-        if (lo != ~0ull) {
-            atomicMin(&t_lo, lo);
-            atomicMax(&t_hi, hi);
-        }
-        __syncthreads();
+    } else if (tid == kStatRows) {
+        goal_s = ld_agent(a.goal_g);
+    } else if (tid == kStatRows + 1) {
+        cur_s = ld_agent(&ctl->cur_b);
+    } else if (tid >= kStatRows + 2 && tid < kStatRows + 5) {
+        const unsigned long long *o[3] = {&st->ovf_near, &st->ovf_far, &st->ovf_out};
+        ovf[tid - kStatRows - 2] = ld_agent(o[tid - kStatRows - 2]);
     }
+    __syncthreads();
     if (tid == 0) {
-        if (ctl->timing && ctl->n_batch && t_hi > t_lo) {
-            ctl->expand_ticks += t_hi - t_lo;
-            ctl->timed_launches++;
-        }
-        ctl->expanded += st->expanded;
-        ctl->reopen += st->reopen;
-        ctl->generated += st->generated;
-        ctl->claimed += st->claimed;
-        ctl->dropped += st->dropped;
+        ctl->expanded += sums[kStExpanded];
+        ctl->reopen += sums[kStReopen];
+        ctl->generated += sums[kStGenerated];
+        ctl->claimed += sums[kStClaimed];
+        ctl->dropped += sums[kStDropped];
         ctl->parents += ctl->n_batch;
-        int fm = fail_bits(*st);
+        int fm = fail_bits(ovf[0], ovf[1], sums[kStOvfTable], ovf[2]);
         if (ctl->claimed * 10 > ctl->table_slots * 7)
             fm |= kFailTable;
         if (fm) {
@@ -453,13 +469,13 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
     unsigned long long *z = (unsigned long long *)st;
     for (int k = tid; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
         z[k] = 0;
-    const int goal = *(volatile int *)a.goal_g;
+    const int goal = goal_s;
     const int w = ctl->band_log2, f0 = ctl->f0;
     const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
     constexpr int per = kBlock / kSub;  // buckets examined per round
-    for (int b0 = ctl->cur_b; b0 <= limit; b0 += per) {
+    for (int b0 = cur_s; b0 <= limit; b0 += per) {
         const int b = b0 + tid / kSub, sq = tid % kSub;
-        if (b <= limit && a.q->W[b][sq] > a.q->R[b][sq])
+        if (b <= limit && ld_agent(&a.q->W[b][sq]) > a.q->R[b][sq])
             atomicMin(&found, b);
         __syncthreads();
         if (found < kBuckets)
@@ -484,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         const int bb = b + tid / kSub, sq = tid % kSub;
         const bool in = bb <= limit && bb < kBuckets;
         rstart[tid] = in ? a.q->R[bb][sq] : 0;
-        avail[tid] = in ? a.q->W[bb][sq] - rstart[tid] : 0;
+        avail[tid] = in ? ld_agent(&a.q->W[bb][sq]) - rstart[tid] : 0;
     }
     __syncthreads();
     if (tid == 0) {
@@ -521,6 +537,8 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         a.q->R[b + tid / kSub][tid % kSub] = rstart[tid] + take[tid];
 }
 
+__global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a) { select_block(a); }
+
 // Entry i of the current batch (binary search over the range prefix in LDS).
 __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl, const unsigned long long *prefix,
                                              unsigned long long i)
@@ -553,11 +571,18 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int lpn = (1 << n) < 64 ? (1 << n) : 64;
     const int npw = 64 / lpn;
     const int per_block = kWaves * npw;
+    if (ctl->status)
+        return;
     const unsigned long long nb = ctl->n_batch;
-    if (ctl->status || (unsigned long long)blockIdx.x * per_block >= nb)
+    // blocks with work; with an empty batch block 0 still runs the tail
+    // (the fused select of the first step)
+    const unsigned long long nact =
+        nb ? ((nb + per_block - 1) / per_block < gridDim.x ? (nb + per_block - 1) / per_block : gridDim.x) : 1;
+    if (blockIdx.x >= nact)
         return;  // blocks beyond the batch leave at once
-    const bool timing = ctl->timing;
-    const unsigned long long t_begin = timing ? device_clock() : 0;
+    const bool timing = ctl->timing && nb;
+    if (timing && blockIdx.x < kArrive && threadIdx.x == 0)
+        __hip_atomic_store(&a.stamps[blockIdx.x], device_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int npairs = P.npairs;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
@@ -657,25 +682,70 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     ovf = wave_sum(ovf);
     stale = wave_sum(stale);
     if (lane == 0) {
+        unsigned long long *row = stat_row(st, blockIdx.x * kWaves + wave);
         if (expanded)
-            atomicAdd(&st->expanded, expanded);
+            atomicAdd(&row[kStExpanded], expanded);
         if (reopen)
-            atomicAdd(&st->reopen, reopen);
+            atomicAdd(&row[kStReopen], reopen);
         if (generated)
-            atomicAdd(&st->generated, generated);
+            atomicAdd(&row[kStGenerated], generated);
         if (claimed)
-            atomicAdd(&st->claimed, claimed);
+            atomicAdd(&row[kStClaimed], claimed);
         if (ovf)
-            atomicAdd(&st->ovf_table, ovf);
+            atomicAdd(&row[kStOvfTable], ovf);
         if (stale)
-            atomicAdd(&st->dropped, stale);
+            atomicAdd(&row[kStDropped], stale);
     }
+    const bool fuse = ctl->fuse;
+    if (!fuse && !timing)
+        return;
+    // the last block to finish: two-level arrival (blockIdx % kArrive, then
+    // the groups) so that no counter takes more than ~64 arrivals
+    // Everything select reads from this launch is an atomic result (the
+    // step statistics, queue W cursors, goal, cur_b), executed at the memory
+    // side; each wave waits for its own atomics to complete before the
+    // block arrives, and select reads them with coherent (sc1) loads.  No
+    // agent-scope fence: on gfx950 it writes back the whole L2 (buffer_wbl2),
+    // which costs far more than the arrival itself.
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned na = (unsigned)nact;
+        const unsigned sub = blockIdx.x % kArrive;
+        const unsigned nsub = (na - sub + kArrive - 1) / kArrive;
+        const unsigned ngrp = na < (unsigned)kArrive ? na : (unsigned)kArrive;
+        int l = 0;
+        if (__hip_atomic_fetch_add(&ctl->arrive[sub], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1)
+            l = __hip_atomic_fetch_add(&ctl->arrive_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                ngrp - 1;
+        last = l;
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    if (threadIdx.x < kArrive)
+        ctl->arrive[threadIdx.x] = 0;
+    if (threadIdx.x == 0)
+        ctl->arrive_top = 0;
+    unsigned long long t0 = 0;
     if (timing) {
+        __shared__ unsigned long long t_lo;
+        if (threadIdx.x == 0)
+            t_lo = ~0ull;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            a.stamps[2 * blockIdx.x] = t_begin;
-            a.stamps[2 * blockIdx.x + 1] = device_clock();
+        if (threadIdx.x < kArrive && threadIdx.x < nact)
+            atomicMin(&t_lo, ld_agent(&a.stamps[threadIdx.x]));
+        __syncthreads();
+        t0 = t_lo;
+    }
+    if (fuse)
+        select_block(a);
+    if (timing && threadIdx.x == 0) {
+        const unsigned long long t1 = device_clock();
+        if (t1 > t0) {
+            ctl->expand_ticks += t1 - t0;
+            ctl->timed_launches++;
         }
     }
 }
@@ -717,10 +787,11 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);
     if (lane_id() == 0) {
+        unsigned long long *row = stat_row(st, (blockIdx.x * blockDim.x + threadIdx.x) / 64);
         if (claimed)
-            atomicAdd(&st->claimed, claimed);
+            atomicAdd(&row[kStClaimed], claimed);
         if (ovf)
-            atomicAdd(&st->ovf_table, ovf);
+            atomicAdd(&row[kStOvfTable], ovf);
     }
 }
 
@@ -814,26 +885,6 @@ __global__ void lookup_kernel(const uint64_t *__restrict__ table, uint64_t cap_m
     out[0] = 1;
     out[1] = table[(uint64_t)s * SW + KW];
     out[2] = table[(uint64_t)s * SW + KW + 1];
-}
-
-__global__ __launch_bounds__(kBlock) void count_table_kernel(const uint64_t *__restrict__ table, uint64_t nslots, int sw,
-                                                             int kw, unsigned long long *__restrict__ out)
-{
-    unsigned long long used = 0, closed = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += stride) {
-        const uint64_t *s = table + i * sw;
-        if (s[0]) {
-            used++;
-            closed += (int)(uint32_t)s[kw + 1] != kIntMax;
-        }
-    }
-    used = wave_sum(used);
-    closed = wave_sum(closed);
-    if (lane_id() == 0) {
-        atomicAdd(&out[0], used);
-        atomicAdd(&out[1], closed);
-    }
 }
 
 }  // namespace dev

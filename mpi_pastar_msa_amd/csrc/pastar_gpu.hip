@@ -769,7 +769,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         PA_TRY(c->pool.alloc((size_t)chunks * kChunk));
         PA_TRY(c->stats.alloc(1));
         PA_TRY(c->ctl.alloc(1));
-        PA_TRY(c->stamps.alloc(2 * kMaxExpandBlocks));
+        PA_TRY(c->stamps.alloc(kArrive));
         PA_TRY(c->goal.alloc(1));
         if (c->n_shards > 1) {
             const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
@@ -792,7 +792,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
     HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
-    HIP_TRY(hipMemsetAsync(c->stamps.p, 0, sizeof(unsigned long long) * 2 * kMaxExpandBlocks, c->stream));
+    HIP_TRY(hipMemsetAsync(c->stamps.p, 0, sizeof(unsigned long long) * kArrive, c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
     return PASTAR_OK;
 }
@@ -874,6 +874,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     hc.max_steps = cfg.max_steps;
     hc.k_start = ~0ull;
     hc.timing = cfg.profile ? 1 : 0;
+    hc.fuse = G == 1 ? 1 : 0;  // one shard: select runs in the tail of expand
     HIP_TRY(hipMemcpy(c->ctl.p, &hc, sizeof(Ctl), hipMemcpyHostToDevice));
 
     SearchArgs a{};
@@ -919,17 +920,17 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     Ctl h{};
     const double t0 = now_s();
     if (G == 1) {
-        // runs of S steps captured once, replayed until `select` reports
-        // termination; with profiling the expand kernel times itself on the
-        // device clock (event nodes inside a graph cost several microseconds
-        // per step)
+        // one launch per step: expand the batch, and the last block to
+        // finish cuts the next one (the first launch, with an empty batch,
+        // only selects).  Runs of S steps are captured once and replayed
+        // until select reports termination; with profiling the expand kernel
+        // times itself on the device clock (event nodes inside a graph cost
+        // several microseconds per step)
         const int S = 32;
         c->graph_used = false;
         auto enqueue_steps = [&](bool) -> hipError_t {
-            for (int k = 0; k < S; k++) {
-                hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
+            for (int k = 0; k < S; k++)
                 ops.expand(expand_grid, blk, c->stream, a);
-            }
             return hipGetLastError();
         };
         hipGraph_t graph = nullptr;
@@ -1058,16 +1059,16 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     if (goal_g == kIntMax)
         return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
 
-    // table and queue census
+    // open-list census (entries left in the queues); the table needs none:
+    // every claimed slot is a distinct node, every first closing of a node
+    // is an expansion that is not a reopening
     DevBuf<unsigned long long> cnt;
-    PA_TRY(cnt.alloc(3));
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, 24, c->stream));
-    hipLaunchKernelGGL(count_table_kernel, dim3(2048), blk, 0, c->stream, c->table.p, c->nslots, slot_words_rt(c->kw),
-                       c->kw, cnt.p);
-    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt.p + 2);
+    PA_TRY(cnt.alloc(1));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
+    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt.p);
     PA_TRY(check_launch());
-    unsigned long long census[3] = {0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(census, cnt.p, 24, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long open_left = 0;
+    HIP_TRY(hipMemcpyAsync(&open_left, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
 
     std::memset(res, 0, sizeof(*res));
@@ -1075,28 +1076,14 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     res->expansions = (int64_t)h.expanded;
     res->reopen = (int64_t)h.reopen;
     res->generated = (int64_t)h.generated;
-    res->open_size = (int64_t)census[2];
-    res->closed_size = (int64_t)census[1];
-    res->table_used = (int64_t)census[0];
+    res->open_size = (int64_t)open_left;
+    res->closed_size = (int64_t)(h.expanded - h.reopen);
+    res->table_used = (int64_t)h.claimed;
     res->steps = h.steps;
     res->exchanged = exchanged;
     res->seconds = t1 - t0;
     {
-        unsigned long long ticks = h.expand_ticks, timed = h.timed_launches;
-        if (h.timing && h.n_batch) {  // the last launch, not yet reduced by a select
-            std::vector<unsigned long long> st(2 * kMaxExpandBlocks);
-            HIP_TRY(hipMemcpy(st.data(), c->stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
-            unsigned long long lo = ~0ull, hi = 0;
-            for (int k = 0; k < kMaxExpandBlocks; k++)
-                if (st[2 * k]) {
-                    lo = std::min(lo, st[2 * k]);
-                    hi = std::max(hi, st[2 * k + 1]);
-                }
-            if (hi > lo) {
-                ticks += hi - lo;
-                timed++;
-            }
-        }
+        const unsigned long long ticks = h.expand_ticks, timed = h.timed_launches;
         expand_ms = (double)ticks * 1e-5;  // 100 MHz device clock
         launches = h.timing ? (int64_t)timed : (int64_t)h.steps;
     }
