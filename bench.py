@@ -193,6 +193,8 @@ def main():
     exp_all = sum(r.expansions_all for r, _ in results)
     exp_local = sum(r.expansions for r, _ in results)
     kern_ms = sum(r.expand_ms for r, _ in results)
+    select_ms = sum(r.select_ms for r, _ in results)
+    gap_ms = sum(r.gap_ms for r, _ in results)
     launches = sum(r.expand_launches for r, _ in results)
     wall = sum(r.seconds for r, _ in results) / len(results)
     score = results[-1][0].score
@@ -237,6 +239,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "expand_kernel", "bytes_per_expansion": b_exp,
                      "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
+                     "avg_select_tail_us": 1e3 * select_ms / max(launches, 1),
+                     "avg_gap_us": 1e3 * gap_ms / max(launches, 1),
                      "traffic_source": traffic_src},
     }
     if args.workload in SERIAL_EXPANSIONS:

@@ -129,6 +129,11 @@ typedef struct pastar_result {
     int64_t table_slots;    /* node table capacity used                       */
     int64_t pool_entries, subqueue_entries;
     int64_t graph_replay;   /* 1 when the steps ran as hipGraph replays       */
+    double select_ms;       /* profile = 1, one shard: part of expand_ms spent
+                               in the fused select tail                    */
+    double gap_ms;          /* profile = 1, one shard: device idle between
+                               the end of one step and the start of the next
+                               (launch gaps)                               */
 } pastar_result;
 
 typedef struct pastar_ctx pastar_ctx;

@@ -77,6 +77,8 @@ class pastar_result(ctypes.Structure):
         ("pool_entries", ctypes.c_int64),
         ("subqueue_entries", ctypes.c_int64),
         ("graph_replay", ctypes.c_int64),
+        ("select_ms", ctypes.c_double),
+        ("gap_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -251,6 +251,8 @@ struct Ctl {
     // order), the last block to finish takes the earliest stamp and its own
     // end, and sums over the launches
     unsigned long long k_start, k_end, expand_ticks, timed_launches;
+    unsigned long long select_ticks, gap_ticks, prev_end;
+    unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
     int timing;
     int fuse;  // 1: the last expand block also runs select for the next step
     // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
@@ -413,30 +415,83 @@ __device__ __forceinline__ T ld_agent(const T *p)
 // f below its g).  Run by one whole block of kBlock threads: as its own
 // launch (sharded search, where the exchange sits between expand and
 // select) or as the tail of the last expand block (one shard).
-__device__ __forceinline__ void select_block(const SearchArgs &a)
+// The control words select needs that the caller has already loaded (the
+// expand kernel reads them at its start anyway).
+struct SelView {
+    unsigned long long n_batch, kmax, kmin, table_slots;
+    int batch_b, band_log2, f0, timing;
+};
+
+__device__ __forceinline__ SelView load_view(const Ctl *ctl)
+{
+    SelView v;
+    v.n_batch = ctl->n_batch;
+    v.kmax = ctl->kmax;
+    v.kmin = ctl->kmin;
+    v.table_slots = ctl->table_slots;
+    v.batch_b = ctl->batch_b;
+    v.band_log2 = ctl->band_log2;
+    v.f0 = ctl->f0;
+    v.timing = ctl->timing;
+    return v;
+}
+
+// Requires ctl->status == 0 on entry.
+__device__ __forceinline__ void select_block(const SearchArgs &a, const SelView &v)
 {
     Ctl *ctl = a.ctl;
-    if (ctl->status)
-        return;
     StepStats *st = a.stats;
     const int tid = threadIdx.x;
+    constexpr int kWin = kBlock / kSub;  // buckets per scan window
     static_assert(kStatRows == 64, "one wave sums the stat rows");
-    __shared__ int found, goal_s, cur_s;
-    __shared__ unsigned long long avail[kRanges], rstart[kRanges], take[kRanges];
+    static_assert(kWin >= kWide, "the first window covers a batch's buckets");
+    static_assert(kRanges == 128 && kSub % 2 == 0, "one wave cuts the batch, two ranges per lane");
+    __shared__ int found, goal_s, cur_s, fail_s;
+    __shared__ unsigned long long wv[kBlock], rv[kBlock];
     __shared__ unsigned long long sums[kStFields], ovf[3];
-    // one round trip: every word select needs from the finished step
+    const bool prof = v.timing;
+    unsigned long long tp0 = prof ? device_clock() : 0, tp;
+#define PHASE(k)                                      \
+    if (prof && tid == 0) {                           \
+        tp = device_clock();                          \
+        ctl->phase_ticks[k] += tp - tp0;              \
+        tp0 = tp;                                     \
+    }
+    const int w = v.band_log2, f0 = v.f0;
+    const int b_win = v.batch_b;
+
+    // Phase 1, one round trip: the step's statistics, the goal, cur_b, the
+    // running totals, and the cursors of the kWin buckets from the last
+    // batch's first bucket (children never fall below their parent's bucket,
+    // f being monotone under the consistent HPair heuristic; entries from
+    // other shards can, and lower cur_b, which the scan below then starts
+    // from)
+    unsigned long long acc[6];
+    if (tid == 0) {
+        acc[0] = ctl->expanded;
+        acc[1] = ctl->reopen;
+        acc[2] = ctl->generated;
+        acc[3] = ctl->claimed;
+        acc[4] = ctl->dropped;
+        acc[5] = ctl->parents;
+    }
+    {
+        const int bb = b_win + tid / kSub, sq = tid % kSub;
+        wv[tid] = bb < kBuckets ? ld_agent(&a.q->W[bb][sq]) : 0;
+        rv[tid] = bb < kBuckets ? a.q->R[bb][sq] : 0;
+    }
     if (tid < kStatRows) {
-        unsigned long long v[kStFields];
+        unsigned long long sv[kStFields];
 #pragma unroll
         for (int f = 0; f < kStFields; f++)
-            v[f] = ld_agent(&st->row[tid][f]);
+            sv[f] = ld_agent(&st->row[tid][f]);
 #pragma unroll
         for (int f = 0; f < kStFields; f++)
-            v[f] = wave_sum(v[f]);
+            sv[f] = wave_sum(sv[f]);
         if (tid == 0) {
 #pragma unroll
             for (int f = 0; f < kStFields; f++)
-                sums[f] = v[f];
+                sums[f] = sv[f];
         }
     } else if (tid == kStatRows) {
         goal_s = ld_agent(a.goal_g);
@@ -445,99 +500,146 @@ __device__ __forceinline__ void select_block(const SearchArgs &a)
     } else if (tid >= kStatRows + 2 && tid < kStatRows + 5) {
         const unsigned long long *o[3] = {&st->ovf_near, &st->ovf_far, &st->ovf_out};
         ovf[tid - kStatRows - 2] = ld_agent(o[tid - kStatRows - 2]);
+    } else if (tid == kStatRows + 5) {
+        found = kBuckets;
     }
     __syncthreads();
+    PHASE(0)
     if (tid == 0) {
-        ctl->expanded += sums[kStExpanded];
-        ctl->reopen += sums[kStReopen];
-        ctl->generated += sums[kStGenerated];
-        ctl->claimed += sums[kStClaimed];
-        ctl->dropped += sums[kStDropped];
-        ctl->parents += ctl->n_batch;
+        const unsigned long long claimed = acc[3] + sums[kStClaimed];
+        ctl->expanded = acc[0] + sums[kStExpanded];
+        ctl->reopen = acc[1] + sums[kStReopen];
+        ctl->generated = acc[2] + sums[kStGenerated];
+        ctl->claimed = claimed;
+        ctl->dropped = acc[4] + sums[kStDropped];
+        ctl->parents = acc[5] + v.n_batch;
         int fm = fail_bits(ovf[0], ovf[1], sums[kStOvfTable], ovf[2]);
-        if (ctl->claimed * 10 > ctl->table_slots * 7)
+        if (claimed * 10 > v.table_slots * 7)
             fm |= kFailTable;
         if (fm) {
             ctl->fail_mask |= fm;
             ctl->status = 2;
         }
-        found = kBuckets;
+        fail_s = fm;
+    }
+    const int goal = goal_s;
+    const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
+    const int start = cur_s < b_win ? cur_s : b_win;
+    if (start == b_win) {
+        const int bb = b_win + tid / kSub;
+        if (bb <= limit && wv[tid] > rv[tid])
+            atomicMin(&found, bb);
     }
     __syncthreads();
-    if (ctl->status)
+    PHASE(1)
+    if (fail_s)
         return;
     unsigned long long *z = (unsigned long long *)st;
     for (int k = tid; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
         z[k] = 0;
-    const int goal = goal_s;
-    const int w = ctl->band_log2, f0 = ctl->f0;
-    const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
-    constexpr int per = kBlock / kSub;  // buckets examined per round
-    for (int b0 = cur_s; b0 <= limit; b0 += per) {
-        const int b = b0 + tid / kSub, sq = tid % kSub;
-        if (b <= limit && ld_agent(&a.q->W[b][sq]) > a.q->R[b][sq])
-            atomicMin(&found, b);
-        __syncthreads();
-        if (found < kBuckets)
-            break;
+    // Phase 2 (rare): scan on past the window, or from a lower cur_b
+    if (found == kBuckets) {
+        for (int b0 = start == b_win ? b_win + kWin : start; b0 <= limit; b0 += kWin) {
+            const int b = b0 + tid / kSub, sq = tid % kSub;
+            if (b <= limit && ld_agent(&a.q->W[b][sq]) > a.q->R[b][sq])
+                atomicMin(&found, b);
+            __syncthreads();
+            if (found < kBuckets)
+                break;
+        }
     }
     const int b = found;
     if (b >= kBuckets) {
         if (tid == 0) {
             ctl->n_batch = 0;
             ctl->has_work = 0;
-            if (ctl->n_shards == 1)
-                ctl->status = 1;
-            ctl->steps++;
-            if (ctl->max_steps && ctl->steps >= ctl->max_steps && !ctl->status)
-                ctl->status = 3;
+            const long long steps = ctl->steps + 1;
+            ctl->steps = steps;
+            int status = ctl->n_shards == 1 ? 1 : 0;
+            if (ctl->max_steps && steps >= ctl->max_steps && !status)
+                status = 3;
+            if (status)
+                ctl->status = status;
         }
         return;
     }
-    // ranges r = (bucket b + r / kSub, sub-queue r % kSub); a thin batch
-    // (fewer than kmin entries) also takes the next buckets, up to kWide
-    if (tid < kRanges) {
-        const int bb = b + tid / kSub, sq = tid % kSub;
-        const bool in = bb <= limit && bb < kBuckets;
-        rstart[tid] = in ? a.q->R[bb][sq] : 0;
-        avail[tid] = in ? ld_agent(&a.q->W[bb][sq]) - rstart[tid] : 0;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long left = ctl->kmax, pre = 0;
-        int r = 0;
-        for (int wb = 0; wb < kWide; wb++) {
-            if (wb > 0 && pre >= ctl->kmin)
-                break;
-            for (int sq = 0; sq < kSub; sq++, r++) {
-                const unsigned long long t = avail[r] < left ? avail[r] : left;
-                take[r] = t;
-                ctl->b_start[r] = rstart[r];
-                ctl->b_prefix[r] = pre;
-                pre += t;
-                left -= t;
+    PHASE(2)
+    // Cut the batch: ranges r = (bucket b + r / kSub, sub-queue r % kSub),
+    // r = 0..127, in order, at most kmax entries; bucket k > 0 joins only
+    // while the buckets before it hold fewer than kmin entries (a thin
+    // batch pulls the next buckets, up to kWide).  One wave, two
+    // consecutive ranges per lane, a wave prefix sum; cursors already read
+    // in phase 1 are reused.
+    if (tid < 64) {
+        unsigned long long rs[2], av[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int r = 2 * tid + j;
+            const int bb = b + r / kSub, sq = r % kSub;
+            const bool in = bb <= limit && bb < kBuckets;
+            unsigned long long rsv = 0, wr = 0;
+            if (in) {
+                if (start == b_win && bb < b_win + kWin) {
+                    const int wi = (bb - b_win) * kSub + sq;
+                    rsv = rv[wi];
+                    wr = wv[wi];
+                } else {
+                    rsv = a.q->R[bb][sq];
+                    wr = ld_agent(&a.q->W[bb][sq]);
+                }
             }
+            rs[j] = rsv;
+            av[j] = wr - rsv;
         }
-        for (; r < kRanges; r++) {
-            take[r] = 0;
-            ctl->b_start[r] = 0;
-            ctl->b_prefix[r] = pre;
+        const unsigned long long s2 = av[0] + av[1];
+        unsigned long long inc = s2;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(inc, o);
+            if (tid >= o)
+                inc += y;
         }
-        ctl->b_prefix[kRanges] = pre;
-        ctl->n_batch = pre;
-        ctl->batch_b = b;
-        ctl->cur_b = b;
-        ctl->has_work = 1;
-        ctl->steps++;
-        if (ctl->max_steps && ctl->steps >= ctl->max_steps)
-            ctl->status = 3;
+        const unsigned long long ex0 = inc - s2, ex1 = ex0 + av[0];
+        const int k = (2 * tid) / kSub;                       // bucket offset of both ranges
+        const unsigned long long bstart = __shfl(ex0, k * (kSub / 2));  // entries before bucket k
+        const bool incl = k == 0 || bstart < v.kmin;
+        const unsigned long long kmax = v.kmax;
+        const unsigned long long t0 = incl ? (ex0 < kmax ? (av[0] < kmax - ex0 ? av[0] : kmax - ex0) : 0) : 0;
+        const unsigned long long t1 = incl ? (ex1 < kmax ? (av[1] < kmax - ex1 ? av[1] : kmax - ex1) : 0) : 0;
+        const unsigned long long total = wave_sum(t0 + t1);
+        const unsigned long long p0 = incl ? (ex0 < kmax ? ex0 : kmax) : total;
+        const unsigned long long p1 = incl ? (ex1 < kmax ? ex1 : kmax) : total;
+        const int r0 = 2 * tid;
+        ctl->b_start[r0] = t0 ? rs[0] : 0;
+        ctl->b_start[r0 + 1] = t1 ? rs[1] : 0;
+        ctl->b_prefix[r0] = p0;
+        ctl->b_prefix[r0 + 1] = p1;
+        if (t0)
+            a.q->R[b + r0 / kSub][r0 % kSub] = rs[0] + t0;
+        if (t1)
+            a.q->R[b + (r0 + 1) / kSub][(r0 + 1) % kSub] = rs[1] + t1;
+        if (tid == 0) {
+            ctl->b_prefix[kRanges] = total;
+            ctl->n_batch = total;
+            ctl->batch_b = b;
+            ctl->cur_b = b;
+            ctl->has_work = 1;
+            const long long steps = ctl->steps + 1;
+            ctl->steps = steps;
+            if (ctl->max_steps && steps >= ctl->max_steps)
+                ctl->status = 3;
+        }
     }
-    __syncthreads();
-    if (tid < kRanges && take[tid])
-        a.q->R[b + tid / kSub][tid % kSub] = rstart[tid] + take[tid];
+    PHASE(3)
+#undef PHASE
 }
 
-__global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a) { select_block(a); }
+__global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
+{
+    if (a.ctl->status)
+        return;
+    select_block(a, load_view(a.ctl));
+}
 
 // Entry i of the current batch (binary search over the range prefix in LDS).
 __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl, const unsigned long long *prefix,
@@ -573,14 +675,15 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int per_block = kWaves * npw;
     if (ctl->status)
         return;
-    const unsigned long long nb = ctl->n_batch;
+    const SelView view = load_view(ctl);
+    const unsigned long long nb = view.n_batch;
     // blocks with work; with an empty batch block 0 still runs the tail
     // (the fused select of the first step)
     const unsigned long long nact =
         nb ? ((nb + per_block - 1) / per_block < gridDim.x ? (nb + per_block - 1) / per_block : gridDim.x) : 1;
     if (blockIdx.x >= nact)
         return;  // blocks beyond the batch leave at once
-    const bool timing = ctl->timing && nb;
+    const bool timing = view.timing && nb;
     if (timing && blockIdx.x < kArrive && threadIdx.x == 0)
         __hip_atomic_store(&a.stamps[blockIdx.x], device_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int npairs = P.npairs;
@@ -593,7 +696,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     for (int r = threadIdx.x; r <= kRanges; r += blockDim.x)
         prefix[r] = ctl->b_prefix[r];
     StepStats *st = a.stats;
-    const int w = ctl->band_log2, f0 = ctl->f0;
+    const int w = view.band_log2, f0 = view.f0;
     const int bound = *(volatile int *)a.goal_g;
     unsigned long long expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
     const int masks = 1 << n;
@@ -739,13 +842,18 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         __syncthreads();
         t0 = t_lo;
     }
+    const unsigned long long ts = timing ? device_clock() : 0;
     if (fuse)
-        select_block(a);
+        select_block(a, view);
     if (timing && threadIdx.x == 0) {
         const unsigned long long t1 = device_clock();
         if (t1 > t0) {
             ctl->expand_ticks += t1 - t0;
+            ctl->select_ticks += t1 - ts;
             ctl->timed_launches++;
+            if (ctl->prev_end && t0 > ctl->prev_end)
+                ctl->gap_ticks += t0 - ctl->prev_end;
+            ctl->prev_end = t1;
         }
     }
 }

@@ -273,6 +273,7 @@ struct pastar_ctx {
     unsigned long long grown_pool = 0, grown_maxch = 0, grown_outbox = 0;
     int grown_log2 = 0;
     int last_fail_mask = 0;
+    unsigned long long last_pool_chunks = 0;  // chunks the last search took
     bool graph_used = false;
     // per-problem search constants, computed once per context
     bool origin_ready = false;
@@ -1071,6 +1072,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     HIP_TRY(hipMemcpyAsync(&open_left, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
 
+    c->last_pool_chunks = h.pool_top;
     std::memset(res, 0, sizeof(*res));
     res->score = goal_g;
     res->expansions = (int64_t)h.expanded;
@@ -1088,6 +1090,14 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         launches = h.timing ? (int64_t)timed : (int64_t)h.steps;
     }
     res->expand_ms = expand_ms;
+    res->select_ms = (double)h.select_ticks * 1e-5;
+    if (cfg.verbose && cfg.profile) {
+        std::fprintf(stderr, "[pastar] select phases (us/launch):");
+        for (int k = 0; k < 4; k++)
+            std::fprintf(stderr, " %.2f", (double)h.phase_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.timed_launches));
+        std::fprintf(stderr, "\n");
+    }
+    res->gap_ms = (double)h.gap_ticks * 1e-5;
     res->expand_launches = launches;
     res->expand_parents = (int64_t)h.parents;
     int64_t all[1] = {(int64_t)h.expanded};
@@ -1173,6 +1183,15 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
                          mask, cfg.pool_entries, cfg.subqueue_entries, cfg.table_log2, cfg.outbox_cap);
     }
     if (rc == PASTAR_OK) {
+        // size the next search from this one's use, with headroom, so that
+        // a repeated search of similar size does not restart (the table is
+        // grown when 70% full; aim for <= 45%, and 1.5x the chunks used)
+        const unsigned long long want = (unsigned long long)((double)res->table_used / 0.45) + 1;
+        int lg = 10;
+        while (lg < 32 && (1ull << lg) < want)
+            lg++;
+        c->grown_log2 = std::max(c->grown_log2, lg);
+        c->grown_pool = std::max(c->grown_pool, c->last_pool_chunks * (unsigned long long)kChunk * 3 / 2);
         res->capacity_retries = retries;
         res->table_slots = (int64_t)c->nslots;
         res->pool_entries = (int64_t)cfg.pool_entries;

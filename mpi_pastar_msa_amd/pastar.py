@@ -172,6 +172,8 @@ class SearchResult:
     pool_entries: int = 0
     subqueue_entries: int = 0
     graph_replay: int = 0
+    select_ms: float = 0.0
+    gap_ms: float = 0.0
     extra: dict = field(default_factory=dict)
 
 

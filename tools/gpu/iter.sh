@@ -12,7 +12,7 @@ timeout -k 10 300 python bench.py --workload PF08184 --steps 20 --warmup 3 --cpu
 for f in b_default b_kin b_syn8 b_pf; do
 python -c "
 import json,sys;d=json.load(open('gpurun_out/$f.json'));r=d['roofline']
-print('$f', d['config']['workload'], 'value %.3g ms/step %.2f wall %.4f exp %d steps %.0f graph %s avg_us %.1f frac %.4f score_ok %s'%(d['value'],d['ms_per_step'],d['wall_to_optimal_s'],d['expansions_per_search'],d['steps_per_search'],d['graph_replay'],r['avg_launch_us'],r['frac'],d['score_ok']), 'cpu %.3g'%d['cpu_baseline']['value'] if 'cpu_baseline' in d else '')"
+print('$f', d['config']['workload'], 'value %.3g ms/step %.2f wall %.4f exp %d steps %.0f graph %s avg_us %.1f (sel %.1f gap %.1f) frac %.4f score_ok %s'%(d['value'],d['ms_per_step'],d['wall_to_optimal_s'],d['expansions_per_search'],d['steps_per_search'],d['graph_replay'],r['avg_launch_us'],r['avg_select_tail_us'],r['avg_gap_us'],r['frac'],d['score_ok']), 'cpu %.3g'%d['cpu_baseline']['value'] if 'cpu_baseline' in d else '')"
 done
 mkdir -p gpurun_out/iter_prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/iter_prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/iter_prof/bench.json 2> gpurun_out/iter_prof/err.log || { echo prof_fail; tail gpurun_out/iter_prof/err.log; exit 1; }
