@@ -145,6 +145,7 @@ def main():
     ap.add_argument("--table-log2", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0, help="open-list entry pool (0 = engine default)")
     ap.add_argument("--band", type=int, default=0, help="f band of one step (0 = engine default)")
+    ap.add_argument("--depth", type=int, default=0, help="expansion levels per step (0 = engine default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -169,7 +170,7 @@ def main():
     device = env_int("PASTAR_BENCH_DEVICE", local_rank)  # override for single-GPU rehearsals
     engine = Engine(seqs, device=device, n_shards=world, shard_rank=rank, rccl_id=rid)
     opt = PAStarOpt(batch_nodes=args.batch, table_slots_log2=args.table_log2,
-                    pool_entries=args.pool, band=args.band, profile=True)
+                    pool_entries=args.pool, band=args.band, depth=args.depth, profile=True)
 
     def step():
         engine.init()
@@ -228,7 +229,8 @@ def main():
                 else "reference fixture %s" % fasta_name,
         "config": {"workload": args.workload, "baseline_config": cfg_desc, "n_seqs": n,
                    "lengths": [len(s) for s in seqs.seqs], "hash": "FZORDER/12",
-                   "batch_nodes": args.batch or 32768, "parallelism": "shard%d" % world},
+                   "batch_nodes": args.batch or 32768, "depth": args.depth or 4,
+                   "parallelism": "shard%d" % world},
         "score": score,
         "score_ok": score == known,
         "wall_to_optimal_s": wall,

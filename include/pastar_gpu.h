@@ -108,6 +108,11 @@ typedef struct pastar_search_opts {
                                  restarting the search                     */
     int32_t eager;            /* 1: launch every step from the host instead
                                  of replaying a captured hipGraph          */
+    int32_t depth;            /* expansion levels per step: children whose f
+                                 falls in the step's buckets are expanded by
+                                 the same workgroup in the same launch, up to
+                                 depth - 1 more levels (0 = default)       */
+    int32_t pad;
 } pastar_search_opts;
 
 typedef struct pastar_result {

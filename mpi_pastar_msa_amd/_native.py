@@ -53,6 +53,8 @@ class pastar_search_opts(ctypes.Structure):
         ("verbose", ctypes.c_int32),
         ("no_autogrow", ctypes.c_int32),
         ("eager", ctypes.c_int32),
+        ("depth", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
     ]
 
 

@@ -45,7 +45,34 @@ struct DevProblem {
     const int32_t *H;
     const uint8_t *codes;
     const int32_t *sub;  // alpha x alpha
+    // search form of the pair tables: cell (i, j) of pair p holds
+    // {H_p[i][j] * w_p, cost(s_x[i], s_y[j]) * w_p} (cost 0 on the last row
+    // and column, where the reference reads the string's '\0'), so one 8-B
+    // gather serves both g and h
+    const int2 *HC;
 };
+
+// Per-pair constants staged in LDS by every block that expands nodes.
+struct PairConst {
+    int x, y, w, row, lx, ly;
+    int64_t off;
+};
+
+__device__ __forceinline__ void stage_pairs(const DevProblem &P, PairConst *pc)
+{
+    for (int p = threadIdx.x; p < P.npairs; p += blockDim.x) {
+        const int x = P.pair_x[p], y = P.pair_y[p];
+        PairConst k;
+        k.x = x;
+        k.y = y;
+        k.w = P.weight[p];
+        k.row = P.h_row[p];
+        k.lx = P.len[x];
+        k.ly = P.len[y];
+        k.off = P.h_off[p];
+        pc[p] = k;
+    }
+}
 
 struct Entry {  // open-pile entry
     uint32_t slot;
@@ -158,9 +185,26 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
     uint64_t idx = key_hash<KW>(key) & cap_mask;
     for (int probe = 0; probe < kMaxProbe;) {
         uint64_t *s = table + idx * SW;
-        uint64_t w0 = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // one plain (vector) read of the key words and best: it can only lag,
+        // showing 0 for a key word being published or a larger best
+        uint64_t wv[KW + 1];
+        {
+            const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
+            wv[0] = v0.x;
+            if constexpr (KW == 1) {
+                wv[1] = v0.y;
+            } else {
+                const ulonglong2 v1 = *reinterpret_cast<const ulonglong2 *>(s + 2);
+                wv[1] = v0.y;
+                wv[2] = v1.x;
+                if constexpr (KW == 4) {
+                    wv[3] = v1.y;
+                    wv[4] = s[4];
+                }
+            }
+        }
         bool mine = false;
-        if (w0 == 0) {
+        if (wv[0] == 0) {
             const uint64_t prev = atomicCAS((unsigned long long *)s, 0ull, (unsigned long long)key[0]);
             if (prev == 0) {
 #pragma unroll
@@ -169,12 +213,16 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
                 reinterpret_cast<int32_t *>(s + KW + 1)[1] = h;
                 claimed = true;
                 mine = true;
+                wv[KW] = ~0ull;
             } else {
-                w0 = prev;
+                wv[0] = prev;
+#pragma unroll
+                for (int w = 1; w < KW; w++)
+                    wv[w] = 0;  // unknown: re-read below
             }
         }
         if (!mine) {
-            if (w0 != key[0]) {
+            if (wv[0] != key[0]) {
                 idx = (idx + 1) & cap_mask;
                 probe++;
                 continue;
@@ -182,7 +230,9 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
             bool same = true, pending = false;
 #pragma unroll
             for (int w = 1; w < KW; w++) {
-                const uint64_t v = __hip_atomic_load(s + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t v = wv[w];
+                if (v == 0)
+                    v = __hip_atomic_load(s + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 pending |= (v == 0);
                 same &= (v == key[w]);
             }
@@ -195,8 +245,7 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
             }
         }
         const uint64_t packed = ((uint64_t)(uint32_t)g << 32) | (uint32_t)pmask;
-        const uint64_t seen = s[KW];
-        if (packed < seen) {
+        if (packed < wv[KW]) {
             const uint64_t old = atomicMin((unsigned long long *)(s + KW), (unsigned long long)packed);
             improved = (int64_t)(old >> 32) > (int64_t)g || old == ~0ull;
         }
@@ -307,39 +356,43 @@ __device__ __forceinline__ void decode_key(const DevProblem &P, int n, const uin
     }
 }
 
-// Fills terms[q], q = p*4 + c, for q in [glane, 4P) step lpn.
+// Fills terms[q], q = p*4 + c, for q in [glane, 4P) step lpn: one HC
+// gather per term (the c = 3 term also reads the substitution cost of the
+// parent's cell).
 template <int N, int KW>
-__device__ __forceinline__ void stage_terms(const DevProblem &P, int n, int npairs,
+__device__ __forceinline__ void stage_terms(const DevProblem &P, int n, int npairs, const PairConst *pc,
                                             const Parent<N, KW> &par, int2 *terms, int glane, int lpn)
 {
     for (int q = glane; q < 4 * npairs; q += lpn) {
         const int p = q >> 2, c = q & 3;
-        const int x = P.pair_x[p], y = P.pair_y[p], w = P.weight[p];
+        const PairConst k = pc[p];
         int px = 0, py = 0;
 #pragma unroll
         for (int i = 0; i < Parent<N, KW>::NMAX; i++) {
-            if (i == x)
+            if (i == k.x)
                 px = par.pos[i];
-            if (i == y)
+            if (i == k.y)
                 py = par.pos[i];
         }
         const int bx = c >> 1, by = c & 1;
-        int gc, hc = 0;
+        const int2 *cells = P.HC + k.off;
+        int hc = 0;
+        if (px + bx <= k.lx && py + by <= k.ly)
+            hc = cells[(int64_t)(px + bx) * k.row + (py + by)].x;
+        int gc;
         if (c == 3) {
-            const int lx = P.len[x], ly = P.len[y];
-            const int ax = P.codes[P.seq_off[x] + (px < lx ? px : lx)];
-            const int ay = P.codes[P.seq_off[y] + (py < ly ? py : ly)];
-            gc = P.sub[ax * P.alpha + ay];
-        } else if (c == 2) {  // x moves, y idle: open iff y moved into the parent
-            gc = ((par.pmask >> y) & 1) ? P.gap_open : P.gap_ext;
-        } else if (c == 1) {
-            gc = ((par.pmask >> x) & 1) ? P.gap_open : P.gap_ext;
+            gc = cells[(int64_t)px * k.row + py].y;
         } else {
-            gc = P.gap_gap;
+            int g0;
+            if (c == 2)  // x moves, y idle: open iff y moved into the parent
+                g0 = ((par.pmask >> k.y) & 1) ? P.gap_open : P.gap_ext;
+            else if (c == 1)
+                g0 = ((par.pmask >> k.x) & 1) ? P.gap_open : P.gap_ext;
+            else
+                g0 = P.gap_gap;
+            gc = g0 * k.w;
         }
-        if (px + bx <= P.len[x] && py + by <= P.len[y])
-            hc = P.H[P.h_off[p] + (int64_t)(px + bx) * P.h_row[p] + (py + by)];
-        terms[q] = make_int2(gc * w, hc * w);
+        terms[q] = make_int2(gc, hc);
     }
 }
 

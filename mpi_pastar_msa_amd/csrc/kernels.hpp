@@ -29,70 +29,144 @@ __global__ __launch_bounds__(kBlock) void init_table_kernel(uint64_t *__restrict
     }
 }
 
-// ---------------------------------------------------------------------------
-// PairAlign::Align as an anti-diagonal wavefront (PairAlign.cpp:107-171).
-// One workgroup per pair; cell (i, j) depends on (i+1, j), (i, j+1) and
-// (i+1, j+1), so every anti-diagonal i + j = d is independent.  The last
-// three diagonals live in LDS (value + affine direction), indexed by row i;
-// every cell is written once to the pair's H block.
-// ---------------------------------------------------------------------------
-enum { kNoGap = 0, kGapX = 1, kGapY = 2 };
+enum { kNoGap = 0, kGapX = 1, kGapY = 2 };  // PairAlign affine directions
 
-__global__ __launch_bounds__(kBlock) void pairalign_kernel(const DevProblem *__restrict__ Pp, int32_t *__restrict__ H)
+// ---------------------------------------------------------------------------
+// PairAlign::Align (PairAlign.cpp:107-171), one workgroup of kPaWaves
+// wavefronts per pair, no block barriers in the sweep.  Rows are taken in
+// bands of 64 from the bottom, lane l holding row bottom - 63 + l; a band
+// sweeps the columns right to left with lane l lagging 63 - l steps behind
+// lane 63, so the cell below, (i+1, j), is what lane l+1 produced one step
+// earlier (a DPP wave shift) and the diagonal one, (i+1, j+1), the value
+// received the step before.  Band k runs on wave k % kPaWaves and lags band
+// k-1 by 64 steps: lane 63 reads the row below from band k-1's top row in
+// LDS (ring of kPaWaves rows), gated by band k-1's published step count.
+// Writes the pair's H block and its search form HC ({H * w, cost * w}).
+// ---------------------------------------------------------------------------
+constexpr int kPaWaves = 4;
+
+__device__ __forceinline__ int from_lane_above(int v)
+{
+    // lane l receives lane l + 1's value (wave_shl:1; lane 63 gets 0)
+    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+}
+
+__host__ __device__ constexpr size_t pairalign_lds_bytes(int maxl2, int alpha, bool sub_lds)
+{
+    return (size_t)kPaWaves * (maxl2 + 1) * 5 + (size_t)(maxl2 + 1) + (sub_lds ? (size_t)alpha * alpha * 4 : 0) +
+           kPaWaves * 4 + 64;
+}
+
+// SUB_LDS: the distance table is staged in LDS (every read in the sweep is
+// then an LDS read, and the per-step waits never include the stores).
+template <bool SUB_LDS>
+__global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const DevProblem *__restrict__ Pp,
+                                                                       int32_t *__restrict__ H,
+                                                                       int2 *__restrict__ HC)
 {
     const DevProblem &P = *Pp;
     const int p = blockIdx.x;
-    const int x = P.pair_x[p], y = P.pair_y[p];
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const int x = P.pair_x[p], y = P.pair_y[p], wgt = P.weight[p];
     const int L1 = P.len[x], L2 = P.len[y];
     const int GO = P.gap_open, GE = P.gap_ext;
+    const int alpha = P.alpha;
     const uint8_t *s1 = P.codes + P.seq_off[x];
-    const uint8_t *s2 = P.codes + P.seq_off[y];
+    const uint8_t *s2g = P.codes + P.seq_off[y];
     int32_t *M = H + P.h_off[p];
+    int2 *C = HC + P.h_off[p];
     const int W = L2 + 1;
     extern __shared__ int lds[];
-    int *val = lds;                                       // [3][L1 + 1]
-    unsigned char *dir = (unsigned char *)(lds + 3 * (L1 + 1));  // [3][L1 + 1]
-    for (int d = L1 + L2; d >= 0; d--) {
-        const int r0 = d % 3, r1 = (d + 1) % 3, r2 = (d + 2) % 3;
-        const int ilo = d - L2 > 0 ? d - L2 : 0;
-        const int ihi = d < L1 ? d : L1;
-        for (int i = ilo + (int)threadIdx.x; i <= ihi; i += blockDim.x) {
-            const int j = d - i;
-            int m, a;
-            if (i == L1 && j == L2) {
-                m = 0;
-                a = kNoGap;
-            } else if (i == L1) {
-                m = (j == L2 - 1) ? GO : val[r1 * (L1 + 1) + L1] + GE;
-                a = kGapY;
-            } else if (j == L2) {
-                m = (i == L1 - 1) ? GO : val[r1 * (L1 + 1) + i + 1] + GE;
-                a = kGapX;
-            } else {
-                const int down = val[r1 * (L1 + 1) + i + 1];  // (i+1, j)
-                const int adown = dir[r1 * (L1 + 1) + i + 1];
-                const int right = val[r1 * (L1 + 1) + i];     // (i, j+1)
-                const int aright = dir[r1 * (L1 + 1) + i];
-                const int c0 = down + (adown == kGapX ? GE : GO);
-                const int c1 = right + (aright == kGapY ? GE : GO);
-                if (c0 < c1) {
-                    m = c0;
-                    a = kGapX;
-                } else {
-                    m = c1;
-                    a = kGapY;
-                }
-                const int c2 = val[r2 * (L1 + 1) + i + 1] + P.sub[s1[i] * P.alpha + s2[j]];
-                if (c2 < m) {
-                    m = c2;
-                    a = kNoGap;
+    int *bval = lds;                                              // [kPaWaves][L2 + 1] band top rows
+    int *sub = bval + kPaWaves * W;                               // [alpha * alpha] when staged
+    volatile int *progress = sub + (SUB_LDS ? alpha * alpha : 0);  // [kPaWaves] band << 16 | steps done
+    uint8_t *bdir = (uint8_t *)(progress + kPaWaves);             // [kPaWaves][L2 + 1]
+    uint8_t *s2 = bdir + kPaWaves * W;                            // [L2 + 1] codes of sequence y
+    for (int k = threadIdx.x; k <= L2; k += blockDim.x)
+        s2[k] = s2g[k];
+    if (SUB_LDS)
+        for (int k = threadIdx.x; k < alpha * alpha; k += blockDim.x)
+            sub[k] = P.sub[k];
+    if (threadIdx.x < kPaWaves)
+        progress[threadIdx.x] = -1;
+    const int32_t *subp;
+    if constexpr (SUB_LDS)
+        subp = sub;
+    else
+        subp = P.sub;
+    __syncthreads();
+    const int nbands = L1 / 64 + 1;  // rows L1 .. 0
+    for (int band = wave; band < nbands; band += kPaWaves) {
+        const int bottom = L1 - 64 * band;
+        const int i = bottom - (63 - lane);
+        const bool row_ok = i >= 0;
+        const int cx = row_ok ? (int)s1[i] : 0;  // code 0 at i == L1 (string end)
+        const int *crow = subp + cx * alpha;
+        const bool last_row = i == L1, row_above_last = i == L1 - 1;
+        const bool use_lds_below = lane == 63 && band > 0;
+        const int *below = bval + ((band + kPaWaves - 1) % kPaWaves) * W;
+        const uint8_t *belowd = bdir + ((band + kPaWaves - 1) % kPaWaves) * W;
+        int *top = bval + (band % kPaWaves) * W;
+        uint8_t *topd = bdir + (band % kPaWaves) * W;
+        volatile int *prev_progress = progress + (band + kPaWaves - 1) % kPaWaves;
+        volatile int *my_progress = progress + band % kPaWaves;
+        int32_t *Mrow = M + (int64_t)(row_ok ? i : 0) * W;
+        int2 *Crow = C + (int64_t)(row_ok ? i : 0) * W;
+        int m = 0, a = kNoGap;          // this lane's cell of the previous step: (i, j + 1)
+        int down = 0, adown = kNoGap;   // (i + 1, j)
+        int diag = 0;                   // (i + 1, j + 1)
+        int j = L2 + 63 - lane;         // column of step t: L2 - (t - (63 - lane))
+        int cost = (j >= 0 && j <= L2) ? crow[s2[j]] : 0;  // one step ahead
+        const int nsteps = L2 + 64;
+        for (int t = 0; t < nsteps; t++, j--) {
+            if (band > 0 && t <= L2 && (t & 7) == 0) {
+                // lane 63 reads column L2 - t of band - 1's top row, written
+                // by its lane 0 at its step t + 63; one check covers 8 steps
+                const int need = ((band - 1) << 16) | (t + 71 < nsteps ? t + 71 : nsteps);
+                while (*prev_progress < need)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            // row i + 1 at column j: produced last step by the lane above
+            // (lane 63: the previous band's top row); (i + 1, j + 1) is last
+            // step's (i + 1, j).  Branch-free: every lane computes, only
+            // cells inside the table are stored.
+            const bool in = row_ok && j >= 0 && j <= L2;
+            const int jc = j < 0 ? 0 : (j > L2 ? L2 : j);
+            const int m_up = from_lane_above(m), a_up = from_lane_above(a);
+            const int lb = below[jc], lbd = belowd[jc];
+            diag = down;
+            down = use_lds_below ? lb : m_up;
+            adown = use_lds_below ? lbd : a_up;
+            const int cost_here = cost;
+            const int jn = j - 1 < 0 ? 0 : (j - 1 > L2 ? L2 : j - 1);
+            cost = crow[s2[jn]];
+            const int right = m, aright = a;
+            const int c0 = down + (adown == kGapX ? GE : GO);
+            const int c1 = right + (aright == kGapY ? GE : GO);
+            int mm = c0 < c1 ? c0 : c1;
+            int aa = c0 < c1 ? kGapX : kGapY;
+            const int c2 = diag + cost_here;
+            aa = c2 < mm ? kNoGap : aa;
+            mm = c2 < mm ? c2 : mm;
+            const bool last_col = j == L2;
+            // borders (PairAlign.cpp:142-160)
+            const int m_lastcol = row_above_last ? GO : down + GE;
+            const int m_lastrow = (j == L2 - 1) ? GO : right + GE;
+            mm = last_row ? (last_col ? 0 : m_lastrow) : (last_col ? m_lastcol : mm);
+            aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
+            if (in) {
+                m = mm;
+                a = aa;
+                Mrow[j] = mm;
+                Crow[j] = make_int2(mm * wgt, cost_here * wgt);
+                if (lane == 0) {
+                    top[j] = mm;
+                    topd[j] = (uint8_t)aa;
                 }
             }
-            val[r0 * (L1 + 1) + i] = m;
-            dir[r0 * (L1 + 1) + i] = (unsigned char)a;
-            M[(int64_t)i * W + j] = m;
+            if (lane == 0 && ((t & 7) == 7 || t == nsteps - 1))
+                *my_progress = (band << 16) | (t + 1);  // after this step's top-row write
         }
-        __syncthreads();
     }
 }
 
@@ -135,9 +209,12 @@ __global__ __launch_bounds__(kBlock) void expand_api_kernel(const DevProblem *__
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
     __shared__ int2 terms_all[kWaves][kTPerWave];
+    __shared__ PairConst pc[kMaxPairs];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
     const uint64_t gmask = (lpn == 64 ? ~0ull : ((1ull << (lpn & 63)) - 1ull)) << (group * lpn);
     const int per_block = kWaves * npw;
+    stage_pairs(P, pc);
+    __syncthreads();
     for (int chunk = blockIdx.x; chunk * per_block < n_in; chunk += gridDim.x) {
         const int node = chunk * per_block + wave * npw + group;
         const bool active = node < n_in;
@@ -158,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void expand_api_kernel(const DevProblem *__
             }
             par.g = nd.g;
             par.pmask = nd.parent_mask;
-            stage_terms<N, KW>(P, n, npairs, par, terms, glane, lpn);
+            stage_terms<N, KW>(P, n, npairs, pc, par, terms, glane, lpn);
         }
         __syncthreads();
         int64_t run = active ? out_off[node] : 0;
@@ -235,6 +312,9 @@ struct Ctl {
     int f0;         // f of bucket 0 (h of the origin)
     int cur_b;      // lowest bucket that may hold entries (f_min only grows)
     int batch_b;    // first bucket of the current batch
+    int batch_nb;   // buckets the current batch was cut from
+    int depth;      // expansion levels per launch (block-local continuation)
+    int deep_rounds;  // continuation only when a level may take >= this many rounds
     int n_shards;
     int fail_mask;  // kFail* bits of the capacity that ran out
     int has_work;   // select found a live bucket (multi-shard termination)
@@ -253,6 +333,8 @@ struct Ctl {
     unsigned long long k_start, k_end, expand_ticks, timed_launches;
     unsigned long long select_ticks, gap_ticks, prev_end;
     unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
+    unsigned long long body_ticks[8];   // profile: expand phases of block 0 (diagnostics)
+    unsigned long long body_launches;
     int timing;
     int fuse;  // 1: the last expand block also runs select for the next step
     // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
@@ -356,12 +438,26 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
     }
 }
 
+// Block-local continuation queue (LDS): improved children whose f lies in
+// the current batch's buckets are expanded by the same block in the same
+// launch, up to `depth` levels, instead of waiting for the next step.
+constexpr int kLocalCap = 256;
+constexpr int kDeepBlocks = 256;  // block-rounds per continuation level across the chip
+struct LocalPush {
+    Entry *buf;  // nullptr: disabled
+    int *count;
+    int f_limit;
+    int cap;     // entries one level may take (a block's width per round)
+};
+
 // Route one child: relax locally or post it to its owner shard; queue the
-// improved ones.  All lanes of the wave must call it.
+// improved ones (block-local continuation queue first, when it qualifies).
+// All lanes of the wave must call it.
 template <int KW>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
-                                            int m, unsigned long long &claimed, unsigned long long &ovf)
+                                            int m, unsigned long long &claimed, unsigned long long &ovf,
+                                            const LocalPush &lp)
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
@@ -383,7 +479,27 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
     }
     const int f = g + h;
     const Entry e = {(uint32_t)slot, f};
-    queue_append(a, improved, bucket_of(f, f0, w), e, st);
+    bool global = improved;
+    if (lp.buf) {
+        const bool want = improved && f < lp.f_limit;
+        const uint64_t mask = __ballot(want);
+        if (mask) {
+            const int lane = lane_id();
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader)
+                base = atomicAdd(lp.count, __popcll(mask));
+            base = __shfl(base, leader);
+            if (want) {
+                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (pos < lp.cap) {
+                    lp.buf[pos] = e;
+                    global = false;
+                }
+            }
+        }
+    }
+    queue_append(a, global, bucket_of(f, f0, w), e, st);
     if (P.n_shards > 1) {
         const bool remote = valid && !local;
         Remote<KW> rec;
@@ -418,8 +534,8 @@ __device__ __forceinline__ T ld_agent(const T *p)
 // The control words select needs that the caller has already loaded (the
 // expand kernel reads them at its start anyway).
 struct SelView {
-    unsigned long long n_batch, kmax, kmin, table_slots;
-    int batch_b, band_log2, f0, timing;
+    unsigned long long n_batch, kmax, kmin, table_slots, maxch;
+    int batch_b, batch_nb, band_log2, f0, timing, depth;
 };
 
 __device__ __forceinline__ SelView load_view(const Ctl *ctl)
@@ -429,7 +545,10 @@ __device__ __forceinline__ SelView load_view(const Ctl *ctl)
     v.kmax = ctl->kmax;
     v.kmin = ctl->kmin;
     v.table_slots = ctl->table_slots;
+    v.maxch = ctl->maxch;
     v.batch_b = ctl->batch_b;
+    v.batch_nb = ctl->batch_nb;
+    v.depth = ctl->depth;
     v.band_log2 = ctl->band_log2;
     v.f0 = ctl->f0;
     v.timing = ctl->timing;
@@ -603,6 +722,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         const int k = (2 * tid) / kSub;                       // bucket offset of both ranges
         const unsigned long long bstart = __shfl(ex0, k * (kSub / 2));  // entries before bucket k
         const bool incl = k == 0 || bstart < v.kmin;
+        const int n_incl = __popcll(__ballot(incl && (tid % (kSub / 2)) == 0 && b + k <= limit));
         const unsigned long long kmax = v.kmax;
         const unsigned long long t0 = incl ? (ex0 < kmax ? (av[0] < kmax - ex0 ? av[0] : kmax - ex0) : 0) : 0;
         const unsigned long long t1 = incl ? (ex1 < kmax ? (av[1] < kmax - ex1 ? av[1] : kmax - ex1) : 0) : 0;
@@ -622,6 +742,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
             ctl->b_prefix[kRanges] = total;
             ctl->n_batch = total;
             ctl->batch_b = b;
+            ctl->batch_nb = n_incl > 0 ? n_incl : 1;
             ctl->cur_b = b;
             ctl->has_work = 1;
             const long long steps = ctl->steps + 1;
@@ -642,8 +763,8 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
 }
 
 // Entry i of the current batch (binary search over the range prefix in LDS).
-__device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl, const unsigned long long *prefix,
-                                             unsigned long long i)
+__device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const SelView &v, const unsigned long long *prefix,
+                                             const unsigned long long *bstart, unsigned long long i)
 {
     int lo = 0, hi = kRanges - 1;  // last range with prefix[r] <= i
     while (lo < hi) {
@@ -653,12 +774,11 @@ __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const Ctl *ctl
         else
             hi = mid - 1;
     }
-    const int r = lo, bb = ctl->batch_b + r / kSub, sq = r % kSub;
-    const unsigned long long p = ctl->b_start[r] + (i - prefix[r]);
-    const uint32_t c = a.chunk_tab[((size_t)bb * kSub + sq) * ctl->maxch + (p >> kChunkLog2)];
+    const int r = lo, bb = v.batch_b + r / kSub, sq = r % kSub;
+    const unsigned long long p = bstart[r] + (i - prefix[r]);
+    const uint32_t c = a.chunk_tab[((size_t)bb * kSub + sq) * v.maxch + (p >> kChunkLog2)];
     return a.pool[(size_t)(c - 1) * kChunk + (p & (kChunk - 1))];
 }
-
 
 // expand every entry of the batch (worker_inner's dequeue, closed check and
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
@@ -673,9 +793,10 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int lpn = (1 << n) < 64 ? (1 << n) : 64;
     const int npw = 64 / lpn;
     const int per_block = kWaves * npw;
-    if (ctl->status)
-        return;
+    const int status = ctl->status;
     const SelView view = load_view(ctl);
+    if (status)
+        return;
     const unsigned long long nb = view.n_batch;
     // blocks with work; with an empty batch block 0 still runs the tail
     // (the fused select of the first step)
@@ -691,19 +812,35 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
     __shared__ int2 terms_all[kWaves][kTPerWave];
-    __shared__ unsigned long long prefix[kRanges + 1];
+    __shared__ unsigned long long prefix[kRanges + 1], bstart[kRanges];
+    __shared__ PairConst pc[kMaxPairs];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
-    for (int r = threadIdx.x; r <= kRanges; r += blockDim.x)
+    // one round trip: the batch's ranges and the pair constants
+    for (int r = threadIdx.x; r <= kRanges; r += blockDim.x) {
         prefix[r] = ctl->b_prefix[r];
+        if (r < kRanges)
+            bstart[r] = ctl->b_start[r];
+    }
+    stage_pairs(P, pc);
+    const bool bprof = timing && blockIdx.x == 0 && threadIdx.x == 0;
+    unsigned long long bt0 = bprof ? device_clock() : 0, bt;
+#define BPHASE(k)                                     \
+    if (bprof) {                                      \
+        bt = device_clock();                          \
+        ctl->body_ticks[k] += bt - bt0;               \
+        bt0 = bt;                                     \
+    }
     StepStats *st = a.stats;
     const int w = view.band_log2, f0 = view.f0;
     const int bound = *(volatile int *)a.goal_g;
     unsigned long long expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
     const int masks = 1 << n;
     __syncthreads();
-    for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
-        const unsigned long long node = chunk * per_block + wave * npw + group;
-        bool ok = node < nb;
+    BPHASE(0)
+    // expand one parent per lane group: entry -> staleness / closed check ->
+    // pair terms in LDS -> one child mask per lane -> relax + route.  Every
+    // thread of the block calls it (it holds a block barrier).
+    auto process = [&](bool ok, const Entry e, const LocalPush &lp) {
         Parent<N, KW> par_;
         par_.g = 0;
         par_.pmask = 0;
@@ -712,13 +849,13 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         for (int k = 0; k < KW; k++)
             par_.key[k] = 0;
         if (ok) {
-            const Entry e = batch_entry(a, ctl, prefix, node);
             const uint64_t *s = a.table + (uint64_t)e.slot * SW;
 #pragma unroll
             for (int k = 0; k < KW; k++)
                 par_.key[k] = s[k];
             const uint64_t best = s[KW];
-            const int h = (int)(s[KW + 1] >> 32);
+            const uint64_t aux = s[KW + 1];
+            const int h = (int)(aux >> 32);
             par_.g = (int)(best >> 32);
             par_.pmask = (int)(uint32_t)best;
             // an entry is current iff its f is the node's f under the best g
@@ -728,7 +865,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             int verdict = ok ? 1 : 0;
             if (ok && glane == 0) {
                 int *closed = (int *)(a.table + (uint64_t)e.slot * SW + KW + 1);
-                verdict = *closed != kIntMax ? 2 : 1;
+                verdict = (int)(uint32_t)aux != kIntMax ? 2 : 1;
                 *closed = par_.g;
             }
             verdict = __shfl(verdict, leader_lane);
@@ -739,15 +876,17 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
                 stale += !ok;
             }
         }
+        BPHASE(1)
         if (ok) {
             decode_key<N, KW>(P, n, par_.key, par_.pos);
 #pragma unroll
             for (int i = 0; i < Parent<N, KW>::NMAX; i++)
                 if ((N || i < n) && par_.pos[i] >= P.len[i])
                     par_.blocked |= 1 << i;
-            stage_terms<N, KW>(P, n, npairs, par_, terms, glane, lpn);
+            stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
         }
         __syncthreads();
+        BPHASE(2)
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
             bool valid = ok && m >= 1 && m < masks && !(m & par_.blocked);
@@ -774,9 +913,57 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
                     owner = owner_dev<Parent<N, KW>::NMAX>(P, n, cp, P.n_shards);
                 }
             }
-            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf);
+            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp);
         }
         __syncthreads();
+        BPHASE(3)
+    };
+
+    // level 0: this block's share of the batch; levels 1..depth-1: the
+    // children it queued in LDS (double-buffered)
+    // continuation only while the batch leaves most of the chip idle (with
+    // a full grid, deep chains in a few blocks would only stretch the
+    // launch); a level may take R rounds of the block's width, R chosen so
+    // that the blocks together run about kDeepBlocks block-rounds per level
+    // (a round costs ceil(2^N / 64) child passes)
+    const int passes = masks > 64 ? masks / 64 : 1;
+    const unsigned long long rounds = (unsigned long long)kDeepBlocks / (nact * passes);
+    const int depth = rounds >= (unsigned long long)ctl->deep_rounds ? view.depth : 1;
+    const int f_limit = f0 + (int)(((long long)view.batch_b + view.batch_nb) << w);
+    __shared__ Entry lq[2][kLocalCap];
+    __shared__ int lq_count[2];
+    if (threadIdx.x < 2)
+        lq_count[threadIdx.x] = 0;
+    __syncthreads();
+    // one level takes at most kLocalRounds rounds of the block's width, so a
+    // block's chain never outgrows the work of its neighbours
+    const int lq_cap = (unsigned long long)per_block * rounds < (unsigned long long)kLocalCap
+                           ? per_block * (int)rounds : kLocalCap;
+    LocalPush lp{depth > 1 ? lq[0] : nullptr, &lq_count[0], f_limit, lq_cap};
+    for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
+        const unsigned long long node = chunk * per_block + wave * npw + group;
+        const bool ok = node < nb;
+        Entry e{0, 0};
+        if (ok)
+            e = batch_entry(a, view, prefix, bstart, node);
+        process(ok, e, lp);
+    }
+    int cur = 0;
+    for (int lvl = 1; lvl < depth; lvl++) {
+        const int cnt = lq_count[cur] < lq_cap ? lq_count[cur] : lq_cap;  // read after process's barrier
+        if (cnt == 0)
+            break;
+        const int nxt = cur ^ 1;
+        if (threadIdx.x == 0)
+            lq_count[nxt] = 0;
+        __syncthreads();
+        const LocalPush lq_next{lvl + 1 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap};
+        for (int base = 0; base < cnt; base += per_block) {
+            const int idx = base + wave * npw + group;
+            const bool ok = idx < cnt;
+            process(ok, ok ? lq[cur][idx] : Entry{0, 0}, lq_next);
+        }
+        cur = nxt;
     }
     expanded = wave_sum(expanded);
     reopen = wave_sum(reopen);
@@ -813,18 +1000,26 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     __shared__ int last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    BPHASE(4)
     if (threadIdx.x == 0) {
         const unsigned na = (unsigned)nact;
         const unsigned sub = blockIdx.x % kArrive;
         const unsigned nsub = (na - sub + kArrive - 1) / kArrive;
         const unsigned ngrp = na < (unsigned)kArrive ? na : (unsigned)kArrive;
         int l = 0;
-        if (__hip_atomic_fetch_add(&ctl->arrive[sub], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1)
+        if (na <= (unsigned)kArrive)  // few blocks: one level
+            l = __hip_atomic_fetch_add(&ctl->arrive_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == na - 1;
+        else if (__hip_atomic_fetch_add(&ctl->arrive[sub], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 nsub - 1)
             l = __hip_atomic_fetch_add(&ctl->arrive_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                 ngrp - 1;
         last = l;
     }
     __syncthreads();
+    BPHASE(5)
+    if (bprof)
+        ctl->body_launches++;
+#undef BPHASE
     if (!last)
         return;
     if (threadIdx.x < kArrive)
@@ -890,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
             m = r.pmask;
             valid = g + h < bound;
         }
-        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf);
+        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush{nullptr, nullptr, 0, 0});
     }
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -246,6 +247,7 @@ struct pastar_ctx {
     DevProblem hp{};
     DevBuf<DevProblem> dP;
     DevBuf<int32_t> dH;
+    DevBuf<int2> dHC;
     DevBuf<uint8_t> dcodes;
     DevBuf<int32_t> dsub;
     bool heuristic_ready = false;
@@ -275,6 +277,12 @@ struct pastar_ctx {
     int last_fail_mask = 0;
     unsigned long long last_pool_chunks = 0;  // chunks the last search took
     bool graph_used = false;
+    // the captured step graph, reused while the search buffers (and so the
+    // kernel arguments) stay the same: capture + instantiate + destroy cost
+    // ~0.5 ms per search
+    hipGraph_t step_graph = nullptr;
+    hipGraphExec_t step_exec = nullptr;
+    std::vector<unsigned char> step_key;
     // per-problem search constants, computed once per context
     bool origin_ready = false;
     int32_t h0 = 0;
@@ -398,10 +406,12 @@ int setup_problem(pastar_ctx *c, const pastar_problem *p)
         }
 
     PA_TRY(c->dH.alloc((size_t)hoff));
+    PA_TRY(c->dHC.alloc((size_t)hoff));
     PA_TRY(c->dcodes.alloc(codes.size()));
     PA_TRY(c->dsub.alloc(sub.size()));
     PA_TRY(c->dP.alloc(1));
     hp.H = c->dH.p;
+    hp.HC = c->dHC.p;
     hp.codes = c->dcodes.p;
     hp.sub = c->dsub.p;
     HIP_TRY(hipMemcpy(c->dcodes.p, codes.data(), codes.size(), hipMemcpyHostToDevice));
@@ -604,6 +614,10 @@ void pastar_gpu_destroy(pastar_ctx *c)
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     c->tr.reset();
+    if (c->step_exec)
+        (void)hipGraphExecDestroy(c->step_exec);
+    if (c->step_graph)
+        (void)hipGraphDestroy(c->step_graph);
     if (c->h_stats)
         (void)hipHostFree(c->h_stats);
     if (c->h_ctl)
@@ -622,15 +636,27 @@ int pastar_gpu_build_heuristic(pastar_ctx *c)
     if (!c)
         return fail(PASTAR_EINVAL, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
-    int maxl1 = 0;
+    // one wavefront per pair (pairalign_wave_kernel): LDS holds the row
+    // below the current band, the codes of sequence y and, when it fits, the
+    // distance table
+    int maxl2 = 0;
     for (int k = 0; k < c->npairs; k++)
-        maxl1 = std::max(maxl1, c->hp.len[c->hp.pair_x[k]]);
-    const size_t lds = (size_t)3 * (maxl1 + 1) * (sizeof(int) + 1) + 16;
+        maxl2 = std::max(maxl2, c->hp.len[c->hp.pair_y[k]]);
+    const int sub_lds = c->hp.alpha * c->hp.alpha * 4 <= 32 * 1024 ? 1 : 0;
+    if (maxl2 >= 65536 - 64)
+        return fail(PASTAR_EINVAL, "sequence too long for the PairAlign kernel (%d)", maxl2);
+    const size_t lds = pairalign_lds_bytes(maxl2, c->hp.alpha, sub_lds != 0);
     if (lds > 160 * 1024)
-        return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl1);
+        return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl2);
+    const void *fn = sub_lds ? (const void *)pairalign_wave_kernel<true> : (const void *)pairalign_wave_kernel<false>;
     if (lds > 64 * 1024)
-        HIP_TRY(hipFuncSetAttribute((const void *)pairalign_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(pairalign_kernel, dim3(c->npairs), dim3(kBlock), lds, c->stream, c->dP.p, c->dH.p);
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (sub_lds)
+        hipLaunchKernelGGL(pairalign_wave_kernel<true>, dim3(c->npairs), dim3(64 * kPaWaves), lds, c->stream, c->dP.p,
+                           c->dH.p, c->dHC.p);
+    else
+        hipLaunchKernelGGL(pairalign_wave_kernel<false>, dim3(c->npairs), dim3(64 * kPaWaves), lds, c->stream,
+                           c->dP.p, c->dH.p, c->dHC.p);
     PA_TRY(check_launch());
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->heuristic_ready = true;
@@ -745,7 +771,7 @@ namespace {
 struct SearchCfg {
     unsigned long long kmax, kmin, pool_entries, subqueue_entries, outbox_cap;
     int table_log2;
-    int verbose, profile, eager;
+    int verbose, profile, eager, depth;
     int64_t max_steps;
     int64_t band;
 };
@@ -876,6 +902,17 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     hc.k_start = ~0ull;
     hc.timing = cfg.profile ? 1 : 0;
     hc.fuse = G == 1 ? 1 : 0;  // one shard: select runs in the tail of expand
+    hc.depth = cfg.depth;
+    {
+        // block-local continuation pays where an expansion is cheap (few
+        // children, a narrow frontier: PF08184 2x, syn4x200 1.4x) and costs
+        // where the fan-out is wide (kinase neutral at 16 rounds, syn8x400
+        // 1.7x slower at 2): the minimum rounds a level must be allowed
+        // before a launch continues, by N (profiles/r1_depth_sweep.txt)
+        const char *e = std::getenv("PASTAR_DEEP_ROUNDS");  // tuning override
+        hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 4 ? 2 : c->n <= 6 ? 16 : (1 << 30));
+    }
+    hc.batch_nb = 1;
     HIP_TRY(hipMemcpy(c->ctl.p, &hc, sizeof(Ctl), hipMemcpyHostToDevice));
 
     SearchArgs a{};
@@ -934,10 +971,23 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 ops.expand(expand_grid, blk, c->stream, a);
             return hipGetLastError();
         };
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
         bool use_graph = !cfg.eager;
-        if (use_graph) {
+        std::vector<unsigned char> key(sizeof(SearchArgs) + 3 * sizeof(int));
+        {
+            std::memcpy(key.data(), &a, sizeof(SearchArgs));
+            const int extra[3] = {(int)expand_grid.x, c->n, KW};
+            std::memcpy(key.data() + sizeof(SearchArgs), extra, sizeof(extra));
+        }
+        if (use_graph && !(c->step_exec && c->step_key == key)) {
+            if (c->step_exec)
+                (void)hipGraphExecDestroy(c->step_exec);
+            if (c->step_graph)
+                (void)hipGraphDestroy(c->step_graph);
+            c->step_exec = nullptr;
+            c->step_graph = nullptr;
+            c->step_key.clear();
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
             hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
             hipError_t e2 = e == hipSuccess ? enqueue_steps(true) : e;
             hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
@@ -948,15 +998,18 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                     (void)hipGraphExecDestroy(exec);
                 if (graph)
                     (void)hipGraphDestroy(graph);
-                exec = nullptr;
-                graph = nullptr;
                 (void)hipGetLastError();
                 use_graph = false;
                 if (cfg.verbose)
                     std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
                                  hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+            } else {
+                c->step_graph = graph;
+                c->step_exec = exec;
+                c->step_key = key;
             }
         }
+        hipGraphExec_t exec = use_graph ? c->step_exec : nullptr;
         long long steps_before = 0;
         int rc = PASTAR_OK;
         for (;;) {
@@ -980,10 +1033,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                              h.steps, h.expanded, h.cur_b, h.n_batch, h.pool_top);
         }
         c->graph_used = use_graph;
-        if (exec)
-            (void)hipGraphExecDestroy(exec);
-        if (graph)
-            (void)hipGraphDestroy(graph);
         PA_TRY(rc);
     } else {
         for (;;) {
@@ -1095,6 +1144,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::fprintf(stderr, "[pastar] select phases (us/launch):");
         for (int k = 0; k < 4; k++)
             std::fprintf(stderr, " %.2f", (double)h.phase_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.timed_launches));
+        std::fprintf(stderr, "\n[pastar] expand phases of block 0 (us/launch):");
+        for (int k = 0; k < 6; k++)
+            std::fprintf(stderr, " %.2f", (double)h.body_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.body_launches));
         std::fprintf(stderr, "\n");
     }
     res->gap_ms = (double)h.gap_ticks * 1e-5;
@@ -1141,6 +1193,9 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.verbose = o.verbose;
     cfg.profile = o.profile;
     cfg.eager = o.eager;
+    if (o.depth < 0 || o.depth > 64)
+        return fail(PASTAR_EINVAL, "depth %d outside [0, 64]", o.depth);
+    cfg.depth = o.depth > 0 ? o.depth : 8;
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     int rc = PASTAR_OK, retries = 0;

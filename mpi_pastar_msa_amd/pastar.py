@@ -127,12 +127,13 @@ class PAStarOpt:
     verbose: bool = False
     autogrow: bool = True
     eager: bool = False
+    depth: int = 0
 
     def search_opts(self):
         return nat.pastar_search_opts(self.batch_nodes, self.batch_min, self.table_slots_log2, self.pool_entries,
                                       self.subqueue_entries, self.max_steps, self.band, int(self.profile),
                                       int(self.verbose),
-                                      int(not self.autogrow), int(self.eager))
+                                      int(not self.autogrow), int(self.eager), int(self.depth), 0)
 
 
 def compute_weights(seqs):
