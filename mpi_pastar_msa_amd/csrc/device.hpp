@@ -89,7 +89,7 @@ struct StepStats {
     // expanded: parents that passed the stale/closed checks; reopen; generated:
     // border-valid children; claimed: new table slots; dropped: stale or
     // pruned parents; ovf_table: node table probe limit hit
-    unsigned long long row[kStatRows][kStFields];
+    unsigned long long row[kStatRows][2 * kStFields];  // one 128-B line per row
     unsigned long long ovf_near;  // chunk pool exhausted
     unsigned long long ovf_far;   // sub-queue chunk table exhausted
     unsigned long long ovf_out;   // outbox capacity exceeded

@@ -306,56 +306,87 @@ __host__ __device__ inline int fail_bits(unsigned long long near, unsigned long 
     return (near ? kFailNear : 0) | (far ? kFailFar : 0) | (table ? kFailTable : 0) | (out ? kFailOut : 0);
 }
 
+// Device-resident control block.  Grouped by access: the read-mostly words
+// every expand block loads at its start, then each atomically updated word
+// on a cache line of its own (a hot atomic line shared with words that every
+// block reads slows every launch), then the last block's diagnostics.
 struct Ctl {
+    // ---- read by every block, written by select ----
     int status;     // 0 running, 1 done, 2 capacity exhausted, 3 step limit
     int band_log2;  // bucket width = 2^band_log2
     int f0;         // f of bucket 0 (h of the origin)
-    int cur_b;      // lowest bucket that may hold entries (f_min only grows)
     int batch_b;    // first bucket of the current batch
     int batch_nb;   // buckets the current batch was cut from
     int depth;      // expansion levels per launch (block-local continuation)
     int deep_rounds;  // continuation only when a level may take >= this many rounds
     int n_shards;
+    int timing;     // profile bits: 1 launch timing, 2 select phases, 4 expand phases
+    int fuse;       // 1: the last expand block also runs select for the next step
     int fail_mask;  // kFail* bits of the capacity that ran out
     int has_work;   // select found a live bucket (multi-shard termination)
+    int debug;      // 1: select validates its scan start (diagnostics)
+    int pad0;
     unsigned long long kmax;
-    unsigned long long pool_top, pool_chunks, maxch;
+    unsigned long long pool_chunks, maxch;
     unsigned long long table_slots;
     unsigned long long n_batch;
     unsigned long long kmin;  // a batch smaller than this may pull the next buckets
     unsigned long long b_start[kRanges], b_prefix[kRanges + 1];
+    // ---- select's running totals ----
     long long steps, max_steps;
     unsigned long long expanded, reopen, generated, claimed, dropped, parents;
-    // expand-kernel timing on the 100 MHz device clock (s_memrealtime): the
-    // first kArrive blocks stamp their start (blocks are dispatched in index
-    // order), the last block to finish takes the earliest stamp and its own
-    // end, and sums over the launches
-    unsigned long long k_start, k_end, expand_ticks, timed_launches;
+    // ---- atomics, one line each ----
+    alignas(128) unsigned long long pool_top;  // chunk bump allocator
+    alignas(128) int cur_b;  // lowest bucket that may hold entries (f_min only grows)
+    // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
+    // then the groups), reset by the last block
+    alignas(128) unsigned arrive_top;
+    alignas(128) unsigned arrive[kArrive];
+    // ---- last block only: expand-kernel timing on the 100 MHz device clock
+    // (s_memrealtime): the first kArrive blocks stamp their start (blocks are
+    // dispatched in index order), the last block to finish takes the earliest
+    // stamp and its own end, and sums over the launches ----
+    alignas(128) unsigned long long k_start, k_end, expand_ticks, timed_launches;
     unsigned long long select_ticks, gap_ticks, prev_end;
     unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
     unsigned long long body_ticks[8];   // profile: expand phases of block 0 (diagnostics)
     unsigned long long body_launches;
-    int timing;
-    int fuse;  // 1: the last expand block also runs select for the next step
-    // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
-    // then the groups), reset by the last block
-    unsigned arrive_top;
-    unsigned arrive[kArrive];
+    int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step, pad1;
+    unsigned long long dbg_w, dbg_r;
 };
 
 __device__ __forceinline__ unsigned long long device_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
+// Cursor arrays indexed [bucket][sub-queue] but stored sub-queue-major: the
+// 32 sub-queues of one bucket (appended to by blocks of different XCDs at
+// once) sit on 32 different cache lines.
+struct CursorArray {
+    unsigned long long d[kSub][kBuckets];
+    struct Row {
+        unsigned long long *p;
+        __host__ __device__ unsigned long long &operator[](int sq) const { return p[(size_t)sq * kBuckets]; }
+    };
+    struct CRow {
+        const unsigned long long *p;
+        __host__ __device__ const unsigned long long &operator[](int sq) const { return p[(size_t)sq * kBuckets]; }
+    };
+    __host__ __device__ Row operator[](int b) { return Row{&d[0][b]}; }
+    __host__ __device__ CRow operator[](int b) const { return CRow{&d[0][b]}; }
+};
+
 struct Queues {
-    unsigned long long W[kBuckets][kSub];
-    unsigned long long R[kBuckets][kSub];
+    CursorArray W;  // reserved by appends
+    CursorArray R;  // consumed by batches
 };
 
 constexpr int kMaxExpandBlocks = 4096;
+constexpr int kTraceSteps = 4096;
 
 struct SearchArgs {
     const DevProblem *P;
     Ctl *ctl;
     unsigned long long *stamps;  // [kArrive] start stamps of the first blocks
+    int *trace;                  // debug: [kTraceSteps][8] per-step select trace (nullptr: off)
     uint64_t *table;
     uint64_t cap_mask;
     Queues *q;
@@ -373,6 +404,23 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     for (int o = 32; o > 0; o >>= 1)
         v += __shfl_xor(v, o);
     return v;
+}
+
+// Loads of words other blocks of the same launch update with atomics (the
+// fused select runs in the last expand block): coherent across XCDs.
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Stores to words that other launches update with atomics (cursors, cur_b,
+// counters): atomic too, so that a plain store's copy in one XCD's L2 can
+// never land over a later atomic update from another XCD.
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int bucket_of(int f, int f0, int w)
@@ -415,7 +463,10 @@ __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, 
 
 // Wave-aggregated append of the predicated lanes' entries to their buckets:
 // one atomic per distinct bucket in the wave.  Every lane must call it.
-__device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int b, const Entry &e, StepStats *st)
+// may_lower: entries can land below cur_b (records from other shards; a
+// shard's own children never fall below the bucket of their parent).
+__device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int b, const Entry &e, StepStats *st,
+                                             bool may_lower)
 {
     const int sq = blockIdx.x % kSub;
     const int lane = lane_id();
@@ -428,8 +479,15 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
         if (lane == leader) {
             base = atomicAdd(&a.q->W[bl][sq], (unsigned long long)__popcll(m));
             // entries from other shards may land below this shard's minimum
-            if (bl < a.ctl->cur_b)
+            if (may_lower && bl < ld_agent(&a.ctl->cur_b))
                 atomicMin(&a.ctl->cur_b, bl);
+#ifdef PASTAR_TRACE_APPENDS
+            if (a.trace) {
+                const long long stp = ld_agent(&a.ctl->steps);
+                if (stp < kTraceSteps)
+                    atomicMin(&a.trace[stp * 8 + 6], bl);  // lowest bucket appended after select `stp`
+            }
+#endif
         }
         base = __shfl(base, leader);
         if ((m >> lane) & 1ull)
@@ -457,7 +515,7 @@ template <int KW>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned long long &claimed, unsigned long long &ovf,
-                                            const LocalPush &lp)
+                                            const LocalPush &lp, bool remote_in = false)
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
@@ -499,7 +557,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
             }
         }
     }
-    queue_append(a, global, bucket_of(f, f0, w), e, st);
+    queue_append(a, global, bucket_of(f, f0, w), e, st, remote_in);
     if (P.n_shards > 1) {
         const bool remote = valid && !local;
         Remote<KW> rec;
@@ -517,13 +575,6 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
     }
 }
 
-// Loads of words other blocks of the same launch update with atomics (the
-// fused select runs in the last expand block): coherent across XCDs.
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // select: account the previous step, then cut the next batch from the lowest
 // bucket holding entries below the best goal (PAStar::check_stop's
@@ -565,10 +616,10 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     static_assert(kStatRows == 64, "one wave sums the stat rows");
     static_assert(kWin >= kWide, "the first window covers a batch's buckets");
     static_assert(kRanges == 128 && kSub % 2 == 0, "one wave cuts the batch, two ranges per lane");
-    __shared__ int found, goal_s, cur_s, fail_s;
+    __shared__ int found, found2, goal_s, cur_s, fail_s;
     __shared__ unsigned long long wv[kBlock], rv[kBlock];
     __shared__ unsigned long long sums[kStFields], ovf[3];
-    const bool prof = v.timing;
+    const bool prof = v.timing & 2;
     unsigned long long tp0 = prof ? device_clock() : 0, tp;
 #define PHASE(k)                                      \
     if (prof && tid == 0) {                           \
@@ -597,7 +648,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     {
         const int bb = b_win + tid / kSub, sq = tid % kSub;
         wv[tid] = bb < kBuckets ? ld_agent(&a.q->W[bb][sq]) : 0;
-        rv[tid] = bb < kBuckets ? a.q->R[bb][sq] : 0;
+        rv[tid] = bb < kBuckets ? ld_agent(&a.q->R[bb][sq]) : 0;
     }
     if (tid < kStatRows) {
         unsigned long long sv[kStFields];
@@ -621,6 +672,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         ovf[tid - kStatRows - 2] = ld_agent(o[tid - kStatRows - 2]);
     } else if (tid == kStatRows + 5) {
         found = kBuckets;
+        found2 = kBuckets;
     }
     __syncthreads();
     PHASE(0)
@@ -651,23 +703,57 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     }
     __syncthreads();
     PHASE(1)
+    // every wave decides on phase 2 from this value; phase 2 writes its own
+    // found2, so a fast wave's scan cannot change a slow wave's decision
+    const int found1 = found;
     if (fail_s)
         return;
     unsigned long long *z = (unsigned long long *)st;
     for (int k = tid; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
-        z[k] = 0;
+        st_agent(&z[k], 0ull);
+    if (ctl->debug && tid < kSub) {  // diagnostics: entries below the scan start?
+        for (int bb = 0; bb < start; bb++) {
+            const unsigned long long wq = ld_agent(&a.q->W[bb][tid]), rq = ld_agent(&a.q->R[bb][tid]);
+            if (wq > rq) {
+                if (atomicAdd(&ctl->dbg_hits, 1) == 0) {
+                    ctl->dbg_bucket = bb;
+                    ctl->dbg_cur = cur_s;
+                    ctl->dbg_win = b_win;
+                    ctl->dbg_step = (int)ctl->steps;
+                    ctl->dbg_w = wq;
+                    ctl->dbg_r = rq;
+                }
+                break;
+            }
+        }
+    }
     // Phase 2 (rare): scan on past the window, or from a lower cur_b
-    if (found == kBuckets) {
+    int bfound = found1;
+    if (found1 == kBuckets) {
         for (int b0 = start == b_win ? b_win + kWin : start; b0 <= limit; b0 += kWin) {
             const int b = b0 + tid / kSub, sq = tid % kSub;
-            if (b <= limit && ld_agent(&a.q->W[b][sq]) > a.q->R[b][sq])
-                atomicMin(&found, b);
+            if (b <= limit && ld_agent(&a.q->W[b][sq]) > ld_agent(&a.q->R[b][sq]))
+                atomicMin(&found2, b);
             __syncthreads();
-            if (found < kBuckets)
+            bfound = found2;
+            __syncthreads();  // every wave has read it before the next round writes it
+            if (bfound < kBuckets)
                 break;
         }
     }
-    const int b = found;
+    const int b = bfound;
+    if (a.trace && tid == 0) {
+        const long long stp = ctl->steps;
+        if (stp < kTraceSteps) {
+            int *t = a.trace + stp * 8;
+            t[0] = (int)stp;
+            t[1] = cur_s;
+            t[2] = b_win;
+            t[3] = start;
+            t[4] = limit;
+            t[5] = b;
+        }
+    }
     if (b >= kBuckets) {
         if (tid == 0) {
             ctl->n_batch = 0;
@@ -703,7 +789,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
                     rsv = rv[wi];
                     wr = wv[wi];
                 } else {
-                    rsv = a.q->R[bb][sq];
+                    rsv = ld_agent(&a.q->R[bb][sq]);
                     wr = ld_agent(&a.q->W[bb][sq]);
                 }
             }
@@ -735,15 +821,15 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         ctl->b_prefix[r0] = p0;
         ctl->b_prefix[r0 + 1] = p1;
         if (t0)
-            a.q->R[b + r0 / kSub][r0 % kSub] = rs[0] + t0;
+            st_agent(&a.q->R[b + r0 / kSub][r0 % kSub], rs[0] + t0);
         if (t1)
-            a.q->R[b + (r0 + 1) / kSub][(r0 + 1) % kSub] = rs[1] + t1;
+            st_agent(&a.q->R[b + (r0 + 1) / kSub][(r0 + 1) % kSub], rs[1] + t1);
         if (tid == 0) {
             ctl->b_prefix[kRanges] = total;
             ctl->n_batch = total;
             ctl->batch_b = b;
             ctl->batch_nb = n_incl > 0 ? n_incl : 1;
-            ctl->cur_b = b;
+            st_agent(&ctl->cur_b, b);
             ctl->has_work = 1;
             const long long steps = ctl->steps + 1;
             ctl->steps = steps;
@@ -804,7 +890,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         nb ? ((nb + per_block - 1) / per_block < gridDim.x ? (nb + per_block - 1) / per_block : gridDim.x) : 1;
     if (blockIdx.x >= nact)
         return;  // blocks beyond the batch leave at once
-    const bool timing = view.timing && nb;
+    const bool timing = (view.timing & 1) && nb;
     if (timing && blockIdx.x < kArrive && threadIdx.x == 0)
         __hip_atomic_store(&a.stamps[blockIdx.x], device_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int npairs = P.npairs;
@@ -822,7 +908,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             bstart[r] = ctl->b_start[r];
     }
     stage_pairs(P, pc);
-    const bool bprof = timing && blockIdx.x == 0 && threadIdx.x == 0;
+    const bool bprof = (view.timing & 4) && timing && blockIdx.x == 0 && threadIdx.x == 0;
     unsigned long long bt0 = bprof ? device_clock() : 0, bt;
 #define BPHASE(k)                                     \
     if (bprof) {                                      \
@@ -1023,9 +1109,9 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     if (!last)
         return;
     if (threadIdx.x < kArrive)
-        ctl->arrive[threadIdx.x] = 0;
+        st_agent(&ctl->arrive[threadIdx.x], 0u);
     if (threadIdx.x == 0)
-        ctl->arrive_top = 0;
+        st_agent(&ctl->arrive_top, 0u);
     unsigned long long t0 = 0;
     if (timing) {
         __shared__ unsigned long long t_lo;
@@ -1085,7 +1171,8 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
             m = r.pmask;
             valid = g + h < bound;
         }
-        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush{nullptr, nullptr, 0, 0});
+        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush{nullptr, nullptr, 0, 0},
+                        true);
     }
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);
@@ -1098,7 +1185,8 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     }
 }
 
-// Open entries left in the queues (live or stale), for the statistics.
+// Open entries left in the queues (current or superseded), for the
+// statistics: one read of every cursor pair.
 __global__ void queue_census_kernel(const Queues *__restrict__ q, unsigned long long *__restrict__ out)
 {
     unsigned long long s = 0;
@@ -1107,6 +1195,47 @@ __global__ void queue_census_kernel(const Queues *__restrict__ q, unsigned long 
     s = wave_sum(s);
     if (lane_id() == 0 && s)
         atomicAdd(out, s);
+}
+
+// Debug check (PASTAR_DEBUG): open nodes left in the queues: entries that are still current (f equal to
+// the node's best g + h; stale ones are superseded), out[0]; out[1] counts
+// those with f below `goal` (none may remain when the search terminates).
+template <int KW>
+__global__ __launch_bounds__(kBlock) void open_census_kernel(SearchArgs a, int goal, unsigned long long *__restrict__ out)
+{
+    constexpr int SW = slot_words<KW>();
+    const unsigned long long maxch = a.ctl->maxch;
+    unsigned long long live = 0, below = 0;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < kBuckets * kSub; k += gridDim.x * blockDim.x) {
+        const int b = k / kSub, sq = k % kSub;
+        const unsigned long long w = a.q->W[b][sq];
+        for (unsigned long long p = a.q->R[b][sq]; p < w; p++) {
+            if ((p >> kChunkLog2) >= maxch)
+                break;
+            const uint32_t c = a.chunk_tab[((size_t)b * kSub + sq) * maxch + (p >> kChunkLog2)];
+            if (c == 0 || c == kNoChunk)
+                break;
+            const Entry e = a.pool[(size_t)(c - 1) * kChunk + (p & (kChunk - 1))];
+            const uint64_t *slot = a.table + (uint64_t)e.slot * SW;
+            const int g = (int)(slot[KW] >> 32), h = (int)(slot[KW + 1] >> 32);
+            if (g + h == e.f) {
+                live++;
+                below += e.f < goal;
+                if (e.f < goal) {
+                    atomicMin(&out[2], (unsigned long long)e.f);
+                    atomicMin(&out[3], (unsigned long long)b);
+                }
+            }
+        }
+    }
+    live = wave_sum(live);
+    below = wave_sum(below);
+    if (lane_id() == 0) {
+        if (live)
+            atomicAdd(&out[0], live);
+        if (below)
+            atomicAdd(&out[1], below);
+    }
 }
 
 // Backtrace walk (backtrace.cpp:47-69): from `start`, follow parent masks,

@@ -127,7 +127,11 @@ struct Transport {
                                  const unsigned long long *roff, size_t rb, size_t outbox_cap) = 0;
     // device buffer of `root` copied to every shard's same buffer
     virtual int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) = 0;
+    // every shard's `count` host values, concatenated in shard order into
+    // all[G * count] (count <= kGatherMax)
+    virtual int allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all) = 0;
 };
+constexpr int kGatherMax = 16;
 
 }  // namespace
 
@@ -138,7 +142,7 @@ struct pastar_group {
     int arrived = 0;
     long long gen = 0;
     bool broken = false;
-    std::vector<std::array<int64_t, 8>> vals;
+    std::vector<std::array<int64_t, 16>> vals;
     std::vector<std::vector<unsigned long long>> counts;
     std::vector<const uint8_t *> outbox;
     std::vector<void *> bufs;
@@ -212,6 +216,16 @@ class LocalTransport : public Transport {
     int exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
                          const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
+    int allgather(pastar_ctx *, const int64_t *mine, int count, int64_t *all) override
+    {
+        for (int k = 0; k < count; k++)
+            g_->vals[rank_][k] = mine[k];
+        PA_TRY(sync());
+        for (int s2 = 0; s2 < g_->G; s2++)
+            for (int k = 0; k < count; k++)
+                all[s2 * count + k] = g_->vals[s2][k];
+        return sync();
+    }
 
    private:
     pastar_group *g_;
@@ -227,6 +241,7 @@ class RcclTransport : public Transport {
     int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
                          const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
+    int allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all) override;
 
    private:
     ncclComm_t comm_;
@@ -237,6 +252,7 @@ class RcclTransport : public Transport {
 struct pastar_ctx {
     int device = 0, n_shards = 1, shard = 0;
     std::unique_ptr<Transport> tr;  // set when n_shards > 1
+    DevBuf<int64_t> xred;           // RCCL staging of small collectives
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
@@ -599,9 +615,10 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
         ncclComm_t comm = nullptr;
         NCCL_TRY(ncclCommInitRank(&comm, n_shards, id, shard_rank));
         c->tr.reset(new RcclTransport(comm));
+        PA_TRY(c->xred.alloc((size_t)(n_shards + 1) * kGatherMax));
     }
     HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl) + 64, hipHostMallocDefault));  // + pinned scratch
     *out = c.release();
     return PASTAR_OK;
 }
@@ -900,9 +917,17 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     hc.table_slots = c->nslots;
     hc.max_steps = cfg.max_steps;
     hc.k_start = ~0ull;
-    hc.timing = cfg.profile ? 1 : 0;
+    hc.timing = 0;
+    if (cfg.profile) {  // bits: 1 expand launch timing, 2 select phases, 4 expand phases (diagnostics)
+        const char *e = std::getenv("PASTAR_TIMING_MASK");
+        hc.timing = e && *e ? std::atoi(e) : 7;
+    }
     hc.fuse = G == 1 ? 1 : 0;  // one shard: select runs in the tail of expand
     hc.depth = cfg.depth;
+    {
+        const char *e = std::getenv("PASTAR_DEBUG");
+        hc.debug = e && *e ? std::atoi(e) : 0;
+    }
     {
         // block-local continuation pays where an expansion is cheap (few
         // children, a narrow frontier: PF08184 2x, syn4x200 1.4x) and costs
@@ -919,6 +944,16 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
     a.stamps = c->stamps.p;
+    DevBuf<int> trace;
+    a.trace = nullptr;
+    if (hc.debug) {
+        PA_TRY(trace.alloc((size_t)kTraceSteps * 8));
+        std::vector<int> init((size_t)kTraceSteps * 8, 0);
+        for (int k = 0; k < kTraceSteps; k++)
+            init[(size_t)k * 8 + 6] = kBuckets;
+        HIP_TRY(hipMemcpy(trace.p, init.data(), init.size() * 4, hipMemcpyHostToDevice));
+        a.trace = trace.p;
+    }
     a.table = c->table.p;
     a.cap_mask = c->nslots - 1;
     a.q = c->queues.p;
@@ -1035,22 +1070,60 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         c->graph_used = use_graph;
         PA_TRY(rc);
     } else {
+        // one host round trip and one small collective per step: every
+        // shard publishes {records for each shard, goal g, had work, failed}
+        // in a single allgather, then the records move by grouped
+        // point-to-point sends and are relaxed on their owner
+        std::vector<unsigned long long> send(G), recv(G), roff(G + 1);
+        std::vector<int64_t> mine(G + 3), all((size_t)G * (G + 3));
+        int32_t *h_goal = reinterpret_cast<int32_t *>(c->h_ctl + 1);  // pinned scratch after the Ctl copy
         for (;;) {
             hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
             ops.expand(expand_grid, blk, c->stream, a);
             PA_TRY(check_launch());
-            // exchange: counts, then the records (grouped point-to-point over xGMI)
             HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(h_goal, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
             launches++;
-            const int had_work = c->h_ctl->has_work;
-            std::vector<unsigned long long> send(G), recv(G);
+            h = *c->h_ctl;
+            const int goal_local = *h_goal;
             for (int d = 0; d < G; d++)
-                send[d] = std::min<unsigned long long>(c->h_stats->outbox_count[d], cfg.outbox_cap);
-            send[c->shard] = 0;
-            PA_TRY(c->tr->exchange_counts(c, send.data(), recv.data()));
-            std::vector<unsigned long long> roff(G + 1, 0);
+                mine[d] = d == c->shard ? 0 : (int64_t)std::min<unsigned long long>(c->h_stats->outbox_count[d],
+                                                                                     cfg.outbox_cap);
+            mine[G] = goal_local;
+            mine[G + 1] = h.has_work;
+            mine[G + 2] = h.status ? 1 : 0;
+            PA_TRY(c->tr->allgather(c, mine.data(), G + 3, all.data()));
+            int goal_g = goal_local;
+            int64_t any_work = 0, any_fail = 0;
+            for (int sh = 0; sh < G; sh++) {
+                const int64_t *r = &all[(size_t)sh * (G + 3)];
+                recv[sh] = (unsigned long long)r[c->shard];
+                goal_g = std::min<int64_t>(goal_g, r[G]);
+                any_work |= r[G + 1];
+                any_fail |= r[G + 2];
+            }
+            // a capacity failure on any shard stops every shard
+            if (any_fail) {
+                if (!h.status) {
+                    c->last_fail_mask = 0;
+                    return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
+                }
+                break;
+            }
+            // termination: no shard found a live bucket below the best goal
+            // in this step (then nothing was expanded or sent anywhere)
+            if (!any_work)
+                break;
+            if (goal_g < goal_local) {
+                // before insert_remote, whose own finds can only lower it
+                *h_goal = goal_g;
+                HIP_TRY(hipMemcpyAsync(c->goal.p, h_goal, 4, hipMemcpyHostToDevice, c->stream));
+            }
+            for (int d = 0; d < G; d++)
+                send[d] = (unsigned long long)mine[d];
+            roff[0] = 0;
             for (int d = 0; d < G; d++)
                 roff[d + 1] = roff[d] + recv[d];
             PA_TRY(c->tr->exchange_records(c, send.data(), recv.data(), roff.data(), rb, cfg.outbox_cap));
@@ -1062,29 +1135,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 ops.insert_remote(dim3((unsigned)blocks), blk, c->stream, a, c->inbox.p, total);
                 PA_TRY(check_launch());
             }
-            int goal_local = kIntMax;
-            HIP_TRY(hipMemcpyAsync(&goal_local, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            h = *c->h_ctl;
-            // termination: no shard found a live bucket below the best goal
-            // in this step (then nothing was expanded or sent anywhere); a
-            // capacity failure on any shard stops every shard
-            int64_t mn[1] = {goal_local};
-            PA_TRY(allreduce_i64(c, mn, 1, kRedMin));
-            const int goal_g = (int)mn[0];
-            if (goal_g < goal_local)
-                HIP_TRY(hipMemcpy(c->goal.p, &goal_g, 4, hipMemcpyHostToDevice));
-            int64_t st2[2] = {had_work, h.status ? 1 : 0};
-            PA_TRY(allreduce_i64(c, st2, 2, kRedSum));
-            if (st2[1] != 0) {
-                if (!h.status) {
-                    c->last_fail_mask = 0;
-                    return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
-                }
-                break;
-            }
-            if (st2[0] == 0)
-                break;
             if (cfg.verbose && h.steps % 50 == 0)
                 std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %llu bucket %d goal %d\n", c->shard, G,
                              h.steps, h.expanded, h.cur_b, goal_g);
@@ -1109,17 +1159,31 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     if (goal_g == kIntMax)
         return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
 
-    // open-list census (entries left in the queues); the table needs none:
-    // every claimed slot is a distinct node, every first closing of a node
-    // is an expansion that is not a reopening
+    // open-list census (current entries left in the queues); the table
+    // needs none: every claimed slot is a distinct node, every first closing
+    // of a node is an expansion that is not a reopening
     DevBuf<unsigned long long> cnt;
-    PA_TRY(cnt.alloc(1));
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, 8, c->stream));
+    PA_TRY(cnt.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, 24, c->stream));
+    HIP_TRY(hipMemsetAsync(cnt.p + 3, 0xff, 16, c->stream));
     hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt.p);
+    if (hc.debug)  // walks every entry left: debug only
+        hipLaunchKernelGGL(open_census_kernel<KW>, dim3(256), blk, 0, c->stream, a, goal_g, cnt.p + 1);
     PA_TRY(check_launch());
-    unsigned long long open_left = 0;
-    HIP_TRY(hipMemcpyAsync(&open_left, cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long cz[5] = {0, 0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(cz, cnt.p, 40, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned long long open_left = cz[0];
+    const unsigned long long census[4] = {cz[1], cz[2], cz[3], cz[4]};
+    if (census[1]) {
+        Ctl cc;
+        HIP_TRY(hipMemcpy(&cc, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost));
+        std::fprintf(stderr,
+                     "[pastar %d/%d] warning: %llu open nodes below the goal %d at termination (min f %llu bucket "
+                     "%llu; cur_b %d batch_b %d band 2^%d f0 %d steps %lld)\n",
+                     c->shard, G, census[1], goal_g, census[2], census[3], cc.cur_b, cc.batch_b, cc.band_log2, cc.f0,
+                     cc.steps);
+    }
 
     c->last_pool_chunks = h.pool_top;
     std::memset(res, 0, sizeof(*res));
@@ -1379,12 +1443,22 @@ namespace {
 
 int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
 {
-    DevBuf<int64_t> d;
-    PA_TRY(d.alloc((size_t)count));
-    HIP_TRY(hipMemcpyAsync(d.p, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
+    int64_t *d = c->xred.p;  // kGatherMax * 8 values, persistent
+    HIP_TRY(hipMemcpyAsync(d, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
     const ncclRedOp_t nop = op == kRedSum ? ncclSum : (op == kRedMin ? ncclMin : ncclMax);
-    NCCL_TRY(ncclAllReduce(d.p, d.p, (size_t)count, ncclInt64, nop, comm_, c->stream));
-    HIP_TRY(hipMemcpyAsync(vals, d.p, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
+    NCCL_TRY(ncclAllReduce(d, d, (size_t)count, ncclInt64, nop, comm_, c->stream));
+    HIP_TRY(hipMemcpyAsync(vals, d, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
+int RcclTransport::allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all)
+{
+    const int G = c->n_shards;
+    int64_t *d = c->xred.p;  // [G + 1][kGatherMax]: own values, then the gathered ones
+    HIP_TRY(hipMemcpyAsync(d, mine, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
+    NCCL_TRY(ncclAllGather(d, d + kGatherMax, (size_t)count, ncclInt64, comm_, c->stream));
+    HIP_TRY(hipMemcpyAsync(all, d + kGatherMax, sizeof(int64_t) * count * G, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return PASTAR_OK;
 }

@@ -174,3 +174,18 @@ def test_sharded_search_one_gpu(name, shards, kat, oracles):
     assert o.alignment_cost(rows) == ref["score"]
     if "alignment_md5" in ref:
         assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,depth,profile", [(8, 1, True), (4, 0, True), (8, 0, False)])
+def test_sharded_search_repeated_exact(shards, depth, profile, kat):
+    """Regression: a race in select's phase-2 scan (a fast wave's atomicMin on
+    the shared bucket minimum changing a slow wave's decision to scan) let
+    shards skip their lowest bucket and stop early with a worse score, about
+    one search in three at 8 shards with per-launch timing on."""
+    from mpi_pastar_msa_amd import sharded_search
+    ref = kat["inputs"]["syn4x200_s1"]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    for _ in range(4):
+        res, rows = sharded_search(seqs, shards, opt=PAStarOpt(depth=depth, profile=profile))
+        assert [r.score for r in res] == [ref["score"]] * shards
