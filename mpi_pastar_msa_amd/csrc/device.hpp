@@ -245,7 +245,14 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
             }
         }
         const uint64_t packed = ((uint64_t)(uint32_t)g << 32) | (uint32_t)pmask;
-        if (packed < wv[KW]) {
+        if (mine) {
+            // the claimant counts as improving without waiting for the
+            // result: if a racing relaxer already stored a smaller g, this
+            // entry is simply stale (f != best g + h) when popped
+            __hip_atomic_fetch_min((unsigned long long *)(s + KW), (unsigned long long)packed, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            improved = true;
+        } else if (packed < wv[KW]) {
             const uint64_t old = atomicMin((unsigned long long *)(s + KW), (unsigned long long)packed);
             improved = (int64_t)(old >> 32) > (int64_t)g || old == ~0ull;
         }

@@ -499,14 +499,32 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
 // Block-local continuation queue (LDS): improved children whose f lies in
 // the current batch's buckets are expanded by the same block in the same
 // launch, up to `depth` levels, instead of waiting for the next step.
-constexpr int kLocalCap = 256;
+constexpr int kLocalCap = 128;
 constexpr int kDeepBlocks = 256;  // block-rounds per continuation level across the chip
+// A continuation entry carries the parent as relaxed (key, g, h, mask), so
+// the next level needs no table read before it stages the pair terms.
+template <int KW>
+struct LEntry {
+    uint64_t key[KW];
+    uint32_t slot;
+    int g, h, pmask;
+};
+
+template <int KW>
 struct LocalPush {
-    Entry *buf;  // nullptr: disabled
+    LEntry<KW> *buf;  // nullptr: disabled
     int *count;
     int f_limit;
     int cap;     // entries one level may take (a block's width per round)
+    Entry *out;  // block's outgoing buffer for the open list, appended once
+    int *out_n;  // at the end of the launch (nullptr: append at once)
 };
+
+constexpr int kOutCap = 1024;  // entries a block defers to its final append
+
+// Block barrier for LDS data only: outstanding global stores (closed marks,
+// queue entries) need not land before the block moves on.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
@@ -515,7 +533,7 @@ template <int KW>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned long long &claimed, unsigned long long &ovf,
-                                            const LocalPush &lp, bool remote_in = false)
+                                            const LocalPush<KW> &lp, bool remote_in = false)
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
@@ -551,7 +569,33 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProble
             if (want) {
                 const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
                 if (pos < lp.cap) {
-                    lp.buf[pos] = e;
+                    LEntry<KW> le;
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        le.key[k] = ck[k];
+                    le.slot = (uint32_t)slot;
+                    le.g = g;
+                    le.h = h;
+                    le.pmask = m;
+                    lp.buf[pos] = le;
+                    global = false;
+                }
+            }
+        }
+    }
+    if (lp.out) {  // defer to the block's final append (one atomic per bucket and wave there)
+        const uint64_t mask = __ballot(global);
+        if (mask) {
+            const int lane = lane_id();
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader)
+                base = atomicAdd(lp.out_n, __popcll(mask));
+            base = __shfl(base, leader);
+            if (global) {
+                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (pos < kOutCap) {
+                    lp.out[pos] = e;
                     global = false;
                 }
             }
@@ -926,7 +970,9 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     // expand one parent per lane group: entry -> staleness / closed check ->
     // pair terms in LDS -> one child mask per lane -> relax + route.  Every
     // thread of the block calls it (it holds a block barrier).
-    auto process = [&](bool ok, const Entry e, const LocalPush &lp) {
+    // `local`: a continuation entry (parent fields carried in LDS); else a
+    // batch entry {slot, f} whose parent is read from the table
+    auto process = [&](bool ok, const Entry e, const LEntry<KW> &le, bool local, const LocalPush<KW> &lp) {
         Parent<N, KW> par_;
         par_.g = 0;
         par_.pmask = 0;
@@ -934,7 +980,20 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
 #pragma unroll
         for (int k = 0; k < KW; k++)
             par_.key[k] = 0;
-        if (ok) {
+        uint64_t lbest = 0, laux = 0;
+        if (ok && local) {
+#pragma unroll
+            for (int k = 0; k < KW; k++)
+                par_.key[k] = le.key[k];
+            par_.g = le.g;
+            par_.pmask = le.pmask;
+            ok = le.g + le.h < bound;
+            // current-ness and the closed mark are settled after the terms
+            // are staged (these loads overlap the pair-table gathers)
+            const uint64_t *s = a.table + (uint64_t)le.slot * SW;
+            lbest = s[KW];
+            laux = s[KW + 1];
+        } else if (ok) {
             const uint64_t *s = a.table + (uint64_t)e.slot * SW;
 #pragma unroll
             for (int k = 0; k < KW; k++)
@@ -971,7 +1030,26 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
                     par_.blocked |= 1 << i;
             stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
         }
-        __syncthreads();
+        if (local) {  // uniform: a whole level is local or not
+            // current iff nobody has improved the node since it was queued
+            // (a larger or unset best is this block's own update, not yet
+            // landed: the barriers here do not wait for global memory)
+            bool cur = ok && (uint32_t)(lbest >> 32) >= (uint32_t)par_.g;
+            int verdict = cur ? 1 : 0;
+            if (cur && glane == 0) {
+                int *closed = (int *)(a.table + (uint64_t)le.slot * SW + KW + 1);
+                verdict = (int)(uint32_t)laux != kIntMax ? 2 : 1;
+                *closed = par_.g;
+            }
+            verdict = __shfl(verdict, leader_lane);
+            if (glane == 0) {
+                expanded += verdict != 0;
+                reopen += verdict == 2;
+                stale += ok && verdict == 0;
+            }
+            ok = verdict != 0;
+        }
+        lds_barrier();
         BPHASE(2)
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
@@ -1001,7 +1079,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             }
             route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp);
         }
-        __syncthreads();
+        lds_barrier();
         BPHASE(3)
     };
 
@@ -1016,23 +1094,27 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const unsigned long long rounds = (unsigned long long)kDeepBlocks / (nact * passes);
     const int depth = rounds >= (unsigned long long)ctl->deep_rounds ? view.depth : 1;
     const int f_limit = f0 + (int)(((long long)view.batch_b + view.batch_nb) << w);
-    __shared__ Entry lq[2][kLocalCap];
-    __shared__ int lq_count[2];
+    __shared__ LEntry<KW> lq[2][kLocalCap];
+    __shared__ int lq_count[2], out_n;
+    __shared__ Entry outq[kOutCap];
     if (threadIdx.x < 2)
         lq_count[threadIdx.x] = 0;
+    if (threadIdx.x == 0)
+        out_n = 0;
     __syncthreads();
-    // one level takes at most kLocalRounds rounds of the block's width, so a
+    // one level takes at most `rounds` rounds of the block's width, so a
     // block's chain never outgrows the work of its neighbours
     const int lq_cap = (unsigned long long)per_block * rounds < (unsigned long long)kLocalCap
                            ? per_block * (int)rounds : kLocalCap;
-    LocalPush lp{depth > 1 ? lq[0] : nullptr, &lq_count[0], f_limit, lq_cap};
+    LocalPush<KW> lp{depth > 1 ? lq[0] : nullptr, &lq_count[0], f_limit, lq_cap, outq, &out_n};
+    const LEntry<KW> no_le{};
     for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
         const unsigned long long node = chunk * per_block + wave * npw + group;
         const bool ok = node < nb;
         Entry e{0, 0};
         if (ok)
             e = batch_entry(a, view, prefix, bstart, node);
-        process(ok, e, lp);
+        process(ok, e, no_le, false, lp);
     }
     int cur = 0;
     for (int lvl = 1; lvl < depth; lvl++) {
@@ -1042,14 +1124,25 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         const int nxt = cur ^ 1;
         if (threadIdx.x == 0)
             lq_count[nxt] = 0;
-        __syncthreads();
-        const LocalPush lq_next{lvl + 1 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap};
+        lds_barrier();
+        const LocalPush<KW> lq_next{lvl + 1 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap, outq,
+                                    &out_n};
         for (int base = 0; base < cnt; base += per_block) {
             const int idx = base + wave * npw + group;
             const bool ok = idx < cnt;
-            process(ok, ok ? lq[cur][idx] : Entry{0, 0}, lq_next);
+            process(ok, Entry{0, 0}, ok ? lq[cur][idx] : no_le, true, lq_next);
         }
         cur = nxt;
+    }
+    // the deferred open-list entries: one append per bucket and wave
+    {
+        const int no = out_n < kOutCap ? out_n : kOutCap;  // read after the last process barrier
+        for (int base = 0; base < no; base += blockDim.x) {
+            const int i = base + threadIdx.x;
+            const bool has = i < no;
+            const Entry e = has ? outq[i] : Entry{0, 0};
+            queue_append(a, has, bucket_of(e.f, f0, w), e, st, false);
+        }
     }
     expanded = wave_sum(expanded);
     reopen = wave_sum(reopen);
@@ -1171,7 +1264,7 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
             m = r.pmask;
             valid = g + h < bound;
         }
-        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush{nullptr, nullptr, 0, 0},
+        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr},
                         true);
     }
     claimed = wave_sum(claimed);
