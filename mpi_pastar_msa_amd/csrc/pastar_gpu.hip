@@ -296,9 +296,10 @@ struct pastar_ctx {
     // the captured step graph, reused while the search buffers (and so the
     // kernel arguments) stay the same: capture + instantiate + destroy cost
     // ~0.5 ms per search
-    hipGraph_t step_graph = nullptr;
-    hipGraphExec_t step_exec = nullptr;
+    hipGraph_t step_graph[2] = {nullptr, nullptr};
+    hipGraphExec_t step_exec[2] = {nullptr, nullptr};
     std::vector<unsigned char> step_key;
+    long long last_steps = 0;  // steps the last completed search took
     // per-problem search constants, computed once per context
     bool origin_ready = false;
     int32_t h0 = 0;
@@ -631,10 +632,12 @@ void pastar_gpu_destroy(pastar_ctx *c)
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     c->tr.reset();
-    if (c->step_exec)
-        (void)hipGraphExecDestroy(c->step_exec);
-    if (c->step_graph)
-        (void)hipGraphDestroy(c->step_graph);
+    for (int gi = 0; gi < 2; gi++) {
+        if (c->step_exec[gi])
+            (void)hipGraphExecDestroy(c->step_exec[gi]);
+        if (c->step_graph[gi])
+            (void)hipGraphDestroy(c->step_graph[gi]);
+    }
     if (c->h_stats)
         (void)hipHostFree(c->h_stats);
     if (c->h_ctl)
@@ -999,9 +1002,13 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // until select reports termination; with profiling the expand kernel
         // times itself on the device clock (event nodes inside a graph cost
         // several microseconds per step)
-        const int S = 32;
+        // runs of steps captured as two graphs, 32 and 4 launches; the short
+        // one finishes a search whose length the previous search on this
+        // context predicts, so few launches run after termination (each
+        // would only read `status` and leave)
+        constexpr int kLong = 32, kShort = 4;
         c->graph_used = false;
-        auto enqueue_steps = [&](bool) -> hipError_t {
+        auto enqueue_steps = [&](int S) -> hipError_t {
             for (int k = 0; k < S; k++)
                 ops.expand(expand_grid, blk, c->stream, a);
             return hipGetLastError();
@@ -1013,42 +1020,49 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             const int extra[3] = {(int)expand_grid.x, c->n, KW};
             std::memcpy(key.data() + sizeof(SearchArgs), extra, sizeof(extra));
         }
-        if (use_graph && !(c->step_exec && c->step_key == key)) {
-            if (c->step_exec)
-                (void)hipGraphExecDestroy(c->step_exec);
-            if (c->step_graph)
-                (void)hipGraphDestroy(c->step_graph);
-            c->step_exec = nullptr;
-            c->step_graph = nullptr;
-            c->step_key.clear();
-            hipGraph_t graph = nullptr;
-            hipGraphExec_t exec = nullptr;
-            hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
-            hipError_t e2 = e == hipSuccess ? enqueue_steps(true) : e;
-            hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
-            if (e2 == hipSuccess && e3 == hipSuccess)
-                e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-            if (e2 != hipSuccess || e3 != hipSuccess) {
-                if (exec)
-                    (void)hipGraphExecDestroy(exec);
-                if (graph)
-                    (void)hipGraphDestroy(graph);
-                (void)hipGetLastError();
-                use_graph = false;
-                if (cfg.verbose)
-                    std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
-                                 hipGetErrorString(e2 != hipSuccess ? e2 : e3));
-            } else {
-                c->step_graph = graph;
-                c->step_exec = exec;
-                c->step_key = key;
+        if (use_graph && !(c->step_exec[0] && c->step_key == key)) {
+            for (int gi = 0; gi < 2; gi++) {
+                if (c->step_exec[gi])
+                    (void)hipGraphExecDestroy(c->step_exec[gi]);
+                if (c->step_graph[gi])
+                    (void)hipGraphDestroy(c->step_graph[gi]);
+                c->step_exec[gi] = nullptr;
+                c->step_graph[gi] = nullptr;
             }
+            c->step_key.clear();
+            for (int gi = 0; gi < 2 && use_graph; gi++) {
+                hipGraph_t graph = nullptr;
+                hipGraphExec_t exec = nullptr;
+                hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+                hipError_t e2 = e == hipSuccess ? enqueue_steps(gi == 0 ? kLong : kShort) : e;
+                hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
+                if (e2 == hipSuccess && e3 == hipSuccess)
+                    e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+                if (e2 != hipSuccess || e3 != hipSuccess) {
+                    if (exec)
+                        (void)hipGraphExecDestroy(exec);
+                    if (graph)
+                        (void)hipGraphDestroy(graph);
+                    (void)hipGetLastError();
+                    use_graph = false;
+                    if (cfg.verbose)
+                        std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
+                                     hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+                } else {
+                    c->step_graph[gi] = graph;
+                    c->step_exec[gi] = exec;
+                }
+            }
+            if (use_graph)
+                c->step_key = key;
         }
-        hipGraphExec_t exec = use_graph ? c->step_exec : nullptr;
         long long steps_before = 0;
         int rc = PASTAR_OK;
         for (;;) {
-            hipError_t e = use_graph ? hipGraphLaunch(exec, c->stream) : enqueue_steps(false);
+            // long runs until the predicted end is near, then short ones
+            const bool near_end = c->last_steps > 0 && steps_before + kLong > c->last_steps + kShort;
+            const int S = near_end ? kShort : kLong;
+            hipError_t e = use_graph ? hipGraphLaunch(c->step_exec[near_end ? 1 : 0], c->stream) : enqueue_steps(S);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream);
             if (e == hipSuccess)
@@ -1067,6 +1081,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 std::fprintf(stderr, "[pastar] step %lld expanded %llu bucket %d batch %llu pool %llu chunks\n",
                              h.steps, h.expanded, h.cur_b, h.n_batch, h.pool_top);
         }
+        if (h.status == 1)
+            c->last_steps = h.steps;
         c->graph_used = use_graph;
         PA_TRY(rc);
     } else {

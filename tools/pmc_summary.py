@@ -61,6 +61,27 @@ def main():
                 calls += int(row["Calls"])
                 dur += float(row["TotalDurationNs"])
     rocprof_avg_us = dur / calls / 1e3 if calls else None
+    # the same average over the timed searches only: bench.py's steps start
+    # with the PairAlign launch, so the first `warmup` of them are untimed
+    bench_pre = None
+    bpath0 = os.path.join(args.prof, "bench.json")
+    if os.path.exists(bpath0):
+        with open(bpath0) as f:
+            lines0 = [l for l in f if l.startswith("{")]
+        bench_pre = json.loads(lines0[-1]) if lines0 else None
+    timed_avg_us = timed_calls = None
+    trace_path = os.path.join(args.prof, "trace", "run_kernel_trace.csv")
+    if bench_pre and os.path.exists(trace_path):
+        with open(trace_path) as f:
+            rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+        starts = [i for i, r in enumerate(rows) if "pairalign" in r["Kernel_Name"]]
+        warm = bench_pre.get("warmup", 0)
+        if len(starts) > warm:
+            tail = rows[starts[warm]:]
+            d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tail if is_expand(r["Kernel_Name"])]
+            if d:
+                timed_avg_us = sum(d) / len(d) / 1e3
+                timed_calls = len(d)
 
     fetch = per_kernel(os.path.join(args.prof, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(args.prof, "write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -88,6 +109,8 @@ def main():
                       "8-32 B gathers, uncalibrated: read side is an upper bound",
         "rocprof_avg_expand_us": rocprof_avg_us,
         "rocprof_expand_calls": calls,
+        "rocprof_avg_expand_us_timed_searches": timed_avg_us,
+        "rocprof_expand_calls_timed_searches": timed_calls,
         "kernel_stats": os.path.relpath(stats_dst, ROOT),
     }
     if bench:
