@@ -174,10 +174,15 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
 // writes it in the same loop iteration, so no wave can stall on itself).
 // best only decreases, so a lagging read of it can only skip a relaxation
 // that would not improve anything.
+//
+// pre0..2 (KW <= 2, has_pre): the words of the first probe's slot, read by the caller
+// ahead of time (slot_prefetch); a read taken earlier can only lag more,
+// which the protocol already tolerates.
 template <int KW>
 __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t cap_mask,
                                          const uint64_t (&key)[KW], int g, int pmask, int h,
-                                         bool &improved, bool &claimed)
+                                         bool &improved, bool &claimed, bool has_pre = false,
+                                         uint64_t pre0 = 0, uint64_t pre1 = 0, uint64_t pre2 = 0)
 {
     constexpr int SW = slot_words<KW>();
     improved = false;
@@ -188,7 +193,13 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
         // one plain (vector) read of the key words and best: it can only lag,
         // showing 0 for a key word being published or a larger best
         uint64_t wv[KW + 1];
-        {
+        if (KW <= 2 && has_pre) {
+            wv[0] = pre0;
+            wv[1] = pre1;
+            if constexpr (KW == 2)
+                wv[2] = pre2;
+            has_pre = false;
+        } else {
             const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
             wv[0] = v0.x;
             if constexpr (KW == 1) {
@@ -259,6 +270,28 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
         return (int64_t)idx;
     }
     return -1;
+}
+
+// First-probe words of key's slot (key words + best, KW <= 2), for relax's
+// `pre`: issued before the parent's pair terms are staged, so the probe's
+// memory round trip overlaps the pair-table gathers.
+template <int KW>
+struct SlotWords {
+    uint64_t w0, w1, w2;
+};
+
+template <int KW>
+__device__ __forceinline__ SlotWords<KW> slot_prefetch(const uint64_t *__restrict__ table, uint64_t cap_mask,
+                                                       const uint64_t (&key)[KW])
+{
+    static_assert(KW <= 2, "prefetch covers 1- and 2-word keys");
+    constexpr int SW = slot_words<KW>();
+    const uint64_t *s = table + (key_hash<KW>(key) & cap_mask) * SW;
+    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
+    SlotWords<KW> o{v0.x, v0.y, 0};
+    if constexpr (KW == 2)
+        o.w2 = s[2];
+    return o;
 }
 
 // Lookup without insertion (closed list / backtrace).

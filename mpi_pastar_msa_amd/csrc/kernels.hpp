@@ -533,12 +533,13 @@ template <int KW>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned long long &claimed, unsigned long long &ovf,
-                                            const LocalPush<KW> &lp, bool remote_in = false)
+                                            const LocalPush<KW> &lp, bool remote_in = false, bool has_pre = false,
+                                            uint64_t pre0 = 0, uint64_t pre1 = 0, uint64_t pre2 = 0)
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
     if (valid && local) {
-        slot = relax<KW>(a.table, a.cap_mask, ck, g, m, h, improved, cl);
+        slot = relax<KW>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre0, pre1, pre2);
         if (slot < 0) {
             ovf++;
             improved = false;
@@ -917,6 +918,9 @@ template <int N, int KW>
 __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
+    // child-slot prefetch: fixed N (the rounds of 64 children are static)
+    // and 1- or 2-word keys
+    constexpr bool kPf = N > 0 && KW <= 2;
     Ctl *ctl = a.ctl;
     const DevProblem &P = *a.P;
     const int n = N ? N : P.n;
@@ -1022,12 +1026,25 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             }
         }
         BPHASE(1)
+        // first-probe slot words of the first 64 children, read before the
+        // pair terms are staged (one memory round trip less per level)
+        SlotWords<KW <= 2 ? KW : 1> pf{0, 0, 0};
+        bool has_pf = false;
         if (ok) {
             decode_key<N, KW>(P, n, par_.key, par_.pos);
 #pragma unroll
             for (int i = 0; i < Parent<N, KW>::NMAX; i++)
                 if ((N || i < n) && par_.pos[i] >= P.len[i])
                     par_.blocked |= 1 << i;
+            if constexpr (kPf) {
+                const int m = glane;
+                if (m >= 1 && m < masks && !(m & par_.blocked)) {
+                    uint64_t ck[KW];
+                    child_key<N, KW>(P, n, par_.key, m, ck);
+                    pf = slot_prefetch<KW>(a.table, a.cap_mask, ck);
+                    has_pf = true;
+                }
+            }
             stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
         }
         if (local) {  // uniform: a whole level is local or not
@@ -1077,7 +1094,8 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
                     owner = owner_dev<Parent<N, KW>::NMAX>(P, n, cp, P.n_shards);
                 }
             }
-            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp);
+            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp, false,
+                            has_pf && r == 0, pf.w0, pf.w1, pf.w2);
         }
         lds_barrier();
         BPHASE(3)
@@ -1134,14 +1152,53 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         }
         cur = nxt;
     }
-    // the deferred open-list entries: one append per bucket and wave
+    // the deferred open-list entries: ranked per bucket in LDS, then one
+    // cursor atomic per bucket for the whole block, all buckets at once (a
+    // wave-serial loop over buckets costs one dependent round trip each)
     {
+        constexpr int kPer = kOutCap / kBlock;
+        constexpr int kWin = 64;  // buckets above the block's lowest one ranked in LDS
+        __shared__ int fb_min;
+        __shared__ unsigned fb_cnt[kWin];
+        __shared__ unsigned long long fb_base[kWin];
         const int no = out_n < kOutCap ? out_n : kOutCap;  // read after the last process barrier
-        for (int base = 0; base < no; base += blockDim.x) {
-            const int i = base + threadIdx.x;
-            const bool has = i < no;
-            const Entry e = has ? outq[i] : Entry{0, 0};
-            queue_append(a, has, bucket_of(e.f, f0, w), e, st, false);
+        if (no > 0) {  // uniform
+            if (threadIdx.x == 0)
+                fb_min = kBuckets;
+            if (threadIdx.x < kWin)
+                fb_cnt[threadIdx.x] = 0;
+            Entry e[kPer];
+            int bk[kPer], rk[kPer];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                const int i = k * kBlock + threadIdx.x;
+                e[k] = i < no ? outq[i] : Entry{0, 0};
+                bk[k] = i < no ? bucket_of(e[k].f, f0, w) : kBuckets;
+                if (i < no)
+                    atomicMin(&fb_min, bk[k]);
+            }
+            __syncthreads();
+            const int bmin = fb_min;
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                rk[k] = -1;
+                if (k * kBlock + (int)threadIdx.x < no && bk[k] - bmin < kWin)
+                    rk[k] = (int)atomicAdd(&fb_cnt[bk[k] - bmin], 1u);
+            }
+            __syncthreads();
+            const int sq = blockIdx.x % kSub;
+            if (threadIdx.x < kWin && fb_cnt[threadIdx.x])
+                fb_base[threadIdx.x] = atomicAdd(&a.q->W[bmin + threadIdx.x][sq], (unsigned long long)fb_cnt[threadIdx.x]);
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                if (rk[k] >= 0)
+                    queue_store(a, bk[k], sq, fb_base[bk[k] - bmin] + (unsigned long long)rk[k], e[k], st);
+                // beyond the window: the wave-aggregated path
+                const int i = k * kBlock + threadIdx.x;
+                queue_append(a, i < no && rk[k] < 0, bk[k], e[k], st, false);
+            }
         }
     }
     expanded = wave_sum(expanded);
@@ -1276,6 +1333,28 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
         if (ovf)
             atomicAdd(&row[kStOvfTable], ovf);
     }
+}
+
+// Reset the open list between searches: zero the chunk-table entries the
+// last search used (its W cursors say how many chunks each sub-queue took)
+// and then the cursors.  One thread per (bucket, sub-queue); replaces a
+// memset of the whole chunk table (64 MB at the default capacity).
+__global__ void queue_reset_kernel(Queues *__restrict__ q, uint32_t *__restrict__ chunk_tab,
+                                   unsigned long long maxch)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= kBuckets * kSub)
+        return;
+    const int b = k % kBuckets, sq = k / kBuckets;  // sub-queue-major like the cursors
+    const unsigned long long w = q->W[b][sq];
+    unsigned long long used = (w + kChunk - 1) >> kChunkLog2;
+    if (used > maxch)
+        used = maxch;
+    uint32_t *row = chunk_tab + ((size_t)b * kSub + sq) * maxch;
+    for (unsigned long long c = 0; c < used; c++)
+        row[c] = 0;
+    q->W[b][sq] = 0;
+    q->R[b][sq] = 0;
 }
 
 // Open entries left in the queues (current or superseded), for the

@@ -304,6 +304,19 @@ struct pastar_ctx {
     bool origin_ready = false;
     int32_t h0 = 0;
     int auto_band_log2 = 0;
+    // open list known to be consistent (cursors and chunk table as a search
+    // left them), so the next search resets only what it used
+    bool queues_clean_known = false;
+    // node-table size learned from the last search's use (0: none yet)
+    int learned_log2 = 0;
+    // preallocated backtrace buffers (pastar_gpu_alignment)
+    DevBuf<uint64_t> walk_key, walk_last;
+    DevBuf<int32_t> walk_masks;
+    DevBuf<int> walk_info;
+    uint64_t *h_walk = nullptr;  // pinned: key in, {info, masks} out
+    unsigned char *h_stage = nullptr;  // pinned: per-search uploads (Ctl, origin record)
+    DevBuf<uint8_t> seed_rec;          // the origin record of a search
+    DevBuf<unsigned long long> census;  // open-list census of a search
 };
 
 namespace {
@@ -620,6 +633,7 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     }
     HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl) + 64, hipHostMallocDefault));  // + pinned scratch
+    HIP_TRY(hipHostMalloc((void **)&c->h_stage, sizeof(Ctl) + 256, hipHostMallocDefault));
     *out = c.release();
     return PASTAR_OK;
 }
@@ -642,6 +656,10 @@ void pastar_gpu_destroy(pastar_ctx *c)
         (void)hipHostFree(c->h_stats);
     if (c->h_ctl)
         (void)hipHostFree(c->h_ctl);
+    if (c->h_stage)
+        (void)hipHostFree(c->h_stage);
+    if (c->h_walk)
+        (void)hipHostFree(c->h_walk);
     if (c->ev0)
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
@@ -836,8 +854,17 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     else
         hipLaunchKernelGGL((init_table_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
     PA_TRY(check_launch());
-    HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
-    HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
+    if (!same || !c->queues_clean_known) {
+        // fresh buffers: clear everything once
+        HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
+        HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
+        c->queues_clean_known = true;
+    } else {
+        // the chunk-table entries the previous search used, then the cursors
+        hipLaunchKernelGGL(queue_reset_kernel, dim3((kBuckets * kSub + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                           c->stream, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch);
+        PA_TRY(check_launch());
+    }
     HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
     HIP_TRY(hipMemsetAsync(c->stamps.p, 0, sizeof(unsigned long long) * kArrive, c->stream));
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
@@ -941,7 +968,10 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 4 ? 2 : c->n <= 6 ? 16 : (1 << 30));
     }
     hc.batch_nb = 1;
-    HIP_TRY(hipMemcpy(c->ctl.p, &hc, sizeof(Ctl), hipMemcpyHostToDevice));
+    // uploads from pinned staging, stream-ordered (no host round trip
+    // before the first step)
+    std::memcpy(c->h_stage, &hc, sizeof(Ctl));
+    HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
 
     SearchArgs a{};
     a.P = c->dP.p;
@@ -974,8 +1004,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
     // its owner shard, through the same relax path as remote records
     const int origin_owner = G > 1 ? owner_of(c->n, zero, G, c->hp.hash_type, c->hp.hash_shift) : 0;
-    DevBuf<uint8_t> drec;
-    PA_TRY(drec.alloc(rb));
+    if (!c->seed_rec.p)
+        PA_TRY(c->seed_rec.alloc(64));
+    uint8_t *drec = c->seed_rec.p;
     {
         std::vector<uint8_t> rec(rb, 0);
         uint64_t key[4];
@@ -983,13 +1014,16 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::memcpy(rec.data(), key, 8 * KW);
         int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
         std::memcpy(rec.data() + 8 * KW, tail, 16);
-        HIP_TRY(hipMemcpy(drec.p, rec.data(), rb, hipMemcpyHostToDevice));
+        unsigned char *stage = c->h_stage + ((sizeof(Ctl) + 63) / 64) * 64;
+        std::memcpy(stage, rec.data(), rb);
+        HIP_TRY(hipMemcpyAsync(drec, stage, rb, hipMemcpyHostToDevice, c->stream));
     }
     if (c->shard == origin_owner) {
-        ops.insert_remote(dim3(1), blk, c->stream, a, drec.p, 1);
+        ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
         PA_TRY(check_launch());
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (G > 1)
+        HIP_TRY(hipStreamSynchronize(c->stream));
 
     double expand_ms = 0;
     int64_t launches = 0, exchanged = 0;
@@ -1165,8 +1199,23 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     if (h.status == 3)
         return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
-    int goal_g = kIntMax;
-    HIP_TRY(hipMemcpy(&goal_g, c->goal.p, 4, hipMemcpyDeviceToHost));
+    // the goal and the open-list census (current entries left in the
+    // queues; the table needs none: every claimed slot is a distinct node,
+    // every first closing of a node is an expansion that is not a
+    // reopening) in one host round trip
+    if (!c->census.p)
+        PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
+    unsigned long long *cnt = c->census.p;
+    unsigned long long *cz = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
+    int32_t *h_goal_end = reinterpret_cast<int32_t *>(c->h_stage + 128);
+    HIP_TRY(hipMemsetAsync(cnt, 0, 24, c->stream));
+    HIP_TRY(hipMemsetAsync(cnt + 3, 0xff, 16, c->stream));
+    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt);
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int goal_g = *h_goal_end;
     if (G > 1) {
         int64_t mn[1] = {goal_g};
         PA_TRY(allreduce_i64(c, mn, 1, kRedMin));
@@ -1174,21 +1223,12 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     if (goal_g == kIntMax)
         return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
-
-    // open-list census (current entries left in the queues); the table
-    // needs none: every claimed slot is a distinct node, every first closing
-    // of a node is an expansion that is not a reopening
-    DevBuf<unsigned long long> cnt;
-    PA_TRY(cnt.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, 24, c->stream));
-    HIP_TRY(hipMemsetAsync(cnt.p + 3, 0xff, 16, c->stream));
-    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt.p);
-    if (hc.debug)  // walks every entry left: debug only
-        hipLaunchKernelGGL(open_census_kernel<KW>, dim3(256), blk, 0, c->stream, a, goal_g, cnt.p + 1);
-    PA_TRY(check_launch());
-    unsigned long long cz[5] = {0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(cz, cnt.p, 40, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (hc.debug) {  // walks every entry left: debug only
+        hipLaunchKernelGGL(open_census_kernel<KW>, dim3(256), blk, 0, c->stream, a, goal_g, cnt + 1);
+        PA_TRY(check_launch());
+        HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     const unsigned long long open_left = cz[0];
     const unsigned long long census[4] = {cz[1], cz[2], cz[3], cz[4]};
     if (census[1]) {
@@ -1260,7 +1300,10 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     const unsigned long long masks = (1ull << c->n) - 1;
     cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 32768ull;
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
-    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 22;
+    // default node-table size: learned from the last search on this context
+    // (a repeated search of the same problem initialises only what it
+    // needs), else 2^22 slots
+    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : (c->learned_log2 > 0 ? c->learned_log2 : 22);
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
     cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 24);
@@ -1320,12 +1363,13 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     if (rc == PASTAR_OK) {
         // size the next search from this one's use, with headroom, so that
         // a repeated search of similar size does not restart (the table is
-        // grown when 70% full; aim for <= 45%, and 1.5x the chunks used)
-        const unsigned long long want = (unsigned long long)((double)res->table_used / 0.45) + 1;
-        int lg = 10;
+        // grown when 70% full) and probes stay short: load <= 25%, and 1.5x
+        // the chunks used
+        const unsigned long long want = (unsigned long long)((double)res->table_used / 0.25) + 1;
+        int lg = 16;
         while (lg < 32 && (1ull << lg) < want)
             lg++;
-        c->grown_log2 = std::max(c->grown_log2, lg);
+        c->learned_log2 = lg;
         c->grown_pool = std::max(c->grown_pool, c->last_pool_chunks * (unsigned long long)kChunk * 3 / 2);
         res->capacity_retries = retries;
         res->table_slots = (int64_t)c->nslots;
@@ -1377,13 +1421,22 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
     if (stride < total_len + 1)
         return fail(PASTAR_EINVAL, "stride %d < %d", stride, total_len + 1);
     const Ops ops = ops_for(c);
-    DevBuf<uint64_t> dkey, dlast;
-    DevBuf<int32_t> dmasks;
-    DevBuf<int> dinfo;
-    PA_TRY(dkey.alloc(4));
-    PA_TRY(dlast.alloc(4));
-    PA_TRY(dmasks.alloc((size_t)total_len + 1));
-    PA_TRY(dinfo.alloc(2));
+    // walk buffers live on the context (allocated once, grown with the
+    // path length): a backtrace costs no allocation
+    if (!c->walk_key.p)
+        PA_TRY(c->walk_key.alloc(4));
+    if (!c->walk_last.p)
+        PA_TRY(c->walk_last.alloc(4));
+    if (!c->walk_info.p)
+        PA_TRY(c->walk_info.alloc(2));
+    if (c->walk_masks.n < (size_t)total_len + 1)
+        PA_TRY(c->walk_masks.alloc((size_t)total_len + 1));
+    if (!c->h_walk)
+        HIP_TRY(hipHostMalloc((void **)&c->h_walk, 64, hipHostMallocDefault));
+    uint64_t *dkey = c->walk_key.p, *dlast = c->walk_last.p;
+    int32_t *dmasks = c->walk_masks.p;
+    int *dinfo = c->walk_info.p;
+    int *h_info = reinterpret_cast<int *>(c->h_walk + 4);  // pinned: h_walk[0..3] is the key
     // walk from the goal towards the origin; with several shards the walk
     // hops to the owner of each parent (PAStarDistributedBacktrace.cpp:19-213)
     std::vector<uint16_t> pos(PASTAR_MAX_SEQ, 0);
@@ -1401,29 +1454,32 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
         int info[2] = {0, 0};
         std::vector<int32_t> seg;
         if (owner == c->shard) {
-            uint64_t key[4];
-            pack_key(c, pos.data(), key);
-            HIP_TRY(hipMemcpyAsync(dkey.p, key, 32, hipMemcpyHostToDevice, c->stream));
-            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, dkey.p, total_len + 1, G > 1 ? 1 : 0, dmasks.p,
-                     dlast.p, dinfo.p);
+            pack_key(c, pos.data(), c->h_walk);
+            HIP_TRY(hipMemcpyAsync(dkey, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, dkey, total_len + 1, G > 1 ? 1 : 0, dmasks,
+                     dlast, dinfo);
             PA_TRY(check_launch());
-            HIP_TRY(hipMemcpyAsync(info, dinfo.p, 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
+            info[0] = h_info[0];
+            info[1] = h_info[1];
             if (info[1] < 0 || info[1] == 2)
                 return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d)", info[0], info[1]);
         }
         if (G > 1) {
-            PA_TRY(c->tr->broadcast(c, dinfo.p, 8, owner));
-            HIP_TRY(hipMemcpyAsync(info, dinfo.p, 8, hipMemcpyDeviceToHost, c->stream));
+            PA_TRY(c->tr->broadcast(c, dinfo, 8, owner));
+            HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
+            info[0] = h_info[0];
+            info[1] = h_info[1];
             if (info[1] < 0 || info[1] == 2)
                 return fail(PASTAR_ENOTFOUND, "backtrace broken on shard %d", owner);
             if (info[0] > 0)
-                PA_TRY(c->tr->broadcast(c, dmasks.p, 4 * (size_t)info[0], owner));
+                PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)info[0], owner));
         }
         seg.resize((size_t)info[0]);
         if (info[0] > 0)
-            HIP_TRY(hipMemcpyAsync(seg.data(), dmasks.p, 4 * (size_t)info[0], hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(seg.data(), dmasks, 4 * (size_t)info[0], hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         for (int32_t m : seg) {
             path.push_back(m);
