@@ -1335,6 +1335,24 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     }
 }
 
+// The values a shard publishes after its step (sharded search), packed on
+// the device so that the gather of every shard's values is the step's only
+// host round trip: records for each shard (own: 0), goal g, had work, failed.
+__global__ void step_pack_kernel(SearchArgs a, unsigned long long outbox_cap, int64_t *__restrict__ out)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0)
+        return;
+    const Ctl *ctl = a.ctl;
+    const int G = ctl->n_shards, me = a.P->shard;
+    for (int d = 0; d < G; d++) {
+        const unsigned long long k = a.stats->outbox_count[d];
+        out[d] = d == me ? 0 : (int64_t)(k < outbox_cap ? k : outbox_cap);
+    }
+    out[G] = *a.goal_g;
+    out[G + 1] = ctl->has_work;
+    out[G + 2] = ctl->status ? 1 : 0;
+}
+
 // Reset the open list between searches: zero the chunk-table entries the
 // last search used (its W cursors say how many chunks each sub-queue took)
 // and then the cursors.  One thread per (bucket, sub-queue); replaces a

@@ -120,16 +120,16 @@ struct Transport {
     virtual ~Transport() = default;
     // element-wise reduction of host int64 values over all shards
     virtual int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) = 0;
-    // send[d] records go to shard d; recv[s] arrive from shard s
-    virtual int exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv) = 0;
     // outbox segment d -> inbox of shard d at that shard's roff[me]
     virtual int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
                                  const unsigned long long *roff, size_t rb, size_t outbox_cap) = 0;
     // device buffer of `root` copied to every shard's same buffer
     virtual int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) = 0;
-    // every shard's `count` host values, concatenated in shard order into
-    // all[G * count] (count <= kGatherMax)
-    virtual int allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all) = 0;
+    // every shard's `count` device values (dev_mine, written by earlier work
+    // on the context's stream), concatenated in shard order into the host
+    // array all[G * count] (count <= kGatherMax); returns with the stream
+    // drained, so it is the caller's one host round trip
+    virtual int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) = 0;
 };
 constexpr int kGatherMax = 16;
 
@@ -205,18 +205,11 @@ class LocalTransport : public Transport {
         }
         return sync();
     }
-    int exchange_counts(pastar_ctx *, const unsigned long long *send, unsigned long long *recv) override
-    {
-        g_->counts[rank_].assign(send, send + g_->G);
-        PA_TRY(sync());
-        for (int s = 0; s < g_->G; s++)
-            recv[s] = g_->counts[s][rank_];
-        return sync();
-    }
     int exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
                          const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
-    int allgather(pastar_ctx *, const int64_t *mine, int count, int64_t *all) override
+    int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) override;
+    int allgather(const int64_t *mine, int count, int64_t *all)
     {
         for (int k = 0; k < count; k++)
             g_->vals[rank_][k] = mine[k];
@@ -237,11 +230,10 @@ class RcclTransport : public Transport {
     explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
     ~RcclTransport() override { ncclCommDestroy(comm_); }
     int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) override;
-    int exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv) override;
     int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
                          const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
-    int allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all) override;
+    int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) override;
 
    private:
     ncclComm_t comm_;
@@ -280,7 +272,6 @@ struct pastar_ctx {
     DevBuf<int> goal;
     DevBuf<uint8_t> outbox, inbox;
     DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
-    StepStats *h_stats = nullptr;         // pinned
     Ctl *h_ctl = nullptr;                 // pinned
     bool searched = false;
     int64_t score = -1;
@@ -314,9 +305,12 @@ struct pastar_ctx {
     DevBuf<int32_t> walk_masks;
     DevBuf<int> walk_info;
     uint64_t *h_walk = nullptr;  // pinned: key in, {info, masks} out
+    int32_t *h_walk_masks = nullptr;  // pinned: a walked stretch of parent masks
+    size_t h_walk_masks_n = 0;
     unsigned char *h_stage = nullptr;  // pinned: per-search uploads (Ctl, origin record)
     DevBuf<uint8_t> seed_rec;          // the origin record of a search
     DevBuf<unsigned long long> census;  // open-list census of a search
+    unsigned char *h_gather = nullptr;  // pinned: a sharded step's gathered values
 };
 
 namespace {
@@ -631,9 +625,9 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
         c->tr.reset(new RcclTransport(comm));
         PA_TRY(c->xred.alloc((size_t)(n_shards + 1) * kGatherMax));
     }
-    HIP_TRY(hipHostMalloc((void **)&c->h_stats, sizeof(StepStats), hipHostMallocDefault));
     HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl) + 64, hipHostMallocDefault));  // + pinned scratch
     HIP_TRY(hipHostMalloc((void **)&c->h_stage, sizeof(Ctl) + 256, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->h_gather, sizeof(int64_t) * 8 * kGatherMax, hipHostMallocDefault));
     *out = c.release();
     return PASTAR_OK;
 }
@@ -652,14 +646,16 @@ void pastar_gpu_destroy(pastar_ctx *c)
         if (c->step_graph[gi])
             (void)hipGraphDestroy(c->step_graph[gi]);
     }
-    if (c->h_stats)
-        (void)hipHostFree(c->h_stats);
     if (c->h_ctl)
         (void)hipHostFree(c->h_ctl);
     if (c->h_stage)
         (void)hipHostFree(c->h_stage);
     if (c->h_walk)
         (void)hipHostFree(c->h_walk);
+    if (c->h_gather)
+        (void)hipHostFree(c->h_gather);
+    if (c->h_walk_masks)
+        (void)hipHostFree(c->h_walk_masks);
     if (c->ev0)
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
@@ -1125,26 +1121,21 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // in a single allgather, then the records move by grouped
         // point-to-point sends and are relaxed on their owner
         std::vector<unsigned long long> send(G), recv(G), roff(G + 1);
-        std::vector<int64_t> mine(G + 3), all((size_t)G * (G + 3));
+        std::vector<int64_t> all((size_t)G * (G + 3));
         int32_t *h_goal = reinterpret_cast<int32_t *>(c->h_ctl + 1);  // pinned scratch after the Ctl copy
+        int64_t *dmine = c->xred.p;  // [G + 3] packed on the device
         for (;;) {
             hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
             ops.expand(expand_grid, blk, c->stream, a);
+            hipLaunchKernelGGL(step_pack_kernel, dim3(1), dim3(64), 0, c->stream, a,
+                               (unsigned long long)cfg.outbox_cap, dmine);
             PA_TRY(check_launch());
-            HIP_TRY(hipMemcpyAsync(c->h_stats, c->stats.p, sizeof(StepStats), hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipMemcpyAsync(h_goal, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
+            // the step's only host round trip
+            PA_TRY(c->tr->gather_step(c, dmine, G + 3, all.data()));
             launches++;
-            h = *c->h_ctl;
-            const int goal_local = *h_goal;
-            for (int d = 0; d < G; d++)
-                mine[d] = d == c->shard ? 0 : (int64_t)std::min<unsigned long long>(c->h_stats->outbox_count[d],
-                                                                                     cfg.outbox_cap);
-            mine[G] = goal_local;
-            mine[G + 1] = h.has_work;
-            mine[G + 2] = h.status ? 1 : 0;
-            PA_TRY(c->tr->allgather(c, mine.data(), G + 3, all.data()));
+            const int64_t *own = &all[(size_t)c->shard * (G + 3)];
+            const int goal_local = (int)own[G];
+            const bool own_fail = own[G + 2] != 0;
             int goal_g = goal_local;
             int64_t any_work = 0, any_fail = 0;
             for (int sh = 0; sh < G; sh++) {
@@ -1156,7 +1147,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             }
             // a capacity failure on any shard stops every shard
             if (any_fail) {
-                if (!h.status) {
+                if (!own_fail) {
                     c->last_fail_mask = 0;
                     return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
                 }
@@ -1172,7 +1163,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 HIP_TRY(hipMemcpyAsync(c->goal.p, h_goal, 4, hipMemcpyHostToDevice, c->stream));
             }
             for (int d = 0; d < G; d++)
-                send[d] = (unsigned long long)mine[d];
+                send[d] = (unsigned long long)own[d];
             roff[0] = 0;
             for (int d = 0; d < G; d++)
                 roff[d + 1] = roff[d] + recv[d];
@@ -1185,10 +1176,14 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 ops.insert_remote(dim3((unsigned)blocks), blk, c->stream, a, c->inbox.p, total);
                 PA_TRY(check_launch());
             }
-            if (cfg.verbose && h.steps % 50 == 0)
-                std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %llu bucket %d goal %d\n", c->shard, G,
-                             h.steps, h.expanded, h.cur_b, goal_g);
+            if (cfg.verbose && launches % 50 == 0)
+                std::fprintf(stderr, "[pastar %d/%d] step %lld goal %d exchanged %lld\n", c->shard, G,
+                             (long long)launches, goal_g, (long long)exchanged);
         }
+        // the control block once, after the last step (status, totals)
+        HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        h = *c->h_ctl;
     }
     const double t1 = now_s();
     if (h.status == 2) {
@@ -1451,36 +1446,38 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
         if (origin)
             break;
         const int owner = G > 1 ? owner_of(c->n, pos.data(), G, c->hp.hash_type, c->hp.hash_shift) : 0;
-        int info[2] = {0, 0};
-        std::vector<int32_t> seg;
+        // one host round trip per hop: the owner walks its stretch of the
+        // chain, and with several shards the stretch (status, length, masks:
+        // a fixed-size copy, so nobody needs the length first) goes to all
         if (owner == c->shard) {
             pack_key(c, pos.data(), c->h_walk);
             HIP_TRY(hipMemcpyAsync(dkey, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
             ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, dkey, total_len + 1, G > 1 ? 1 : 0, dmasks,
                      dlast, dinfo);
             PA_TRY(check_launch());
-            HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            info[0] = h_info[0];
-            info[1] = h_info[1];
-            if (info[1] < 0 || info[1] == 2)
-                return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d)", info[0], info[1]);
         }
         if (G > 1) {
             PA_TRY(c->tr->broadcast(c, dinfo, 8, owner));
-            HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            info[0] = h_info[0];
-            info[1] = h_info[1];
-            if (info[1] < 0 || info[1] == 2)
-                return fail(PASTAR_ENOTFOUND, "backtrace broken on shard %d", owner);
-            if (info[0] > 0)
-                PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)info[0], owner));
+            PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)(total_len + 1), owner));
         }
-        seg.resize((size_t)info[0]);
-        if (info[0] > 0)
-            HIP_TRY(hipMemcpyAsync(seg.data(), dmasks, 4 * (size_t)info[0], hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
+        if (c->h_walk_masks_n < (size_t)total_len + 1) {
+            if (c->h_walk_masks)
+                (void)hipHostFree(c->h_walk_masks);
+            c->h_walk_masks = nullptr;
+            c->h_walk_masks_n = 0;
+            HIP_TRY(hipHostMalloc((void **)&c->h_walk_masks, 4 * ((size_t)total_len + 1), hipHostMallocDefault));
+            c->h_walk_masks_n = (size_t)total_len + 1;
+        }
+        HIP_TRY(hipMemcpyAsync(c->h_walk_masks, dmasks, 4 * ((size_t)total_len + 1), hipMemcpyDeviceToHost,
+                               c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        const int info[2] = {h_info[0], h_info[1]};
+        if (info[1] < 0 || info[1] == 2)
+            return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d, shard %d)", info[0], info[1], owner);
+        if (info[0] < 0 || info[0] > total_len + 1)
+            return fail(PASTAR_ENOTFOUND, "backtrace stretch of %d steps out of range", info[0]);
+        const std::vector<int32_t> seg(c->h_walk_masks, c->h_walk_masks + info[0]);
         for (int32_t m : seg) {
             path.push_back(m);
             for (int i = 0; i < c->n; i++)
@@ -1524,29 +1521,15 @@ int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
     return PASTAR_OK;
 }
 
-int RcclTransport::allgather(pastar_ctx *c, const int64_t *mine, int count, int64_t *all)
+int RcclTransport::gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all)
 {
     const int G = c->n_shards;
-    int64_t *d = c->xred.p;  // [G + 1][kGatherMax]: own values, then the gathered ones
-    HIP_TRY(hipMemcpyAsync(d, mine, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
-    NCCL_TRY(ncclAllGather(d, d + kGatherMax, (size_t)count, ncclInt64, comm_, c->stream));
-    HIP_TRY(hipMemcpyAsync(all, d + kGatherMax, sizeof(int64_t) * count * G, hipMemcpyDeviceToHost, c->stream));
+    int64_t *d = c->xred.p + kGatherMax;  // [G][kGatherMax] after the own-values row
+    int64_t *h = reinterpret_cast<int64_t *>(c->h_gather);
+    NCCL_TRY(ncclAllGather(dev_mine, d, (size_t)count, ncclInt64, comm_, c->stream));
+    HIP_TRY(hipMemcpyAsync(h, d, sizeof(int64_t) * count * G, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return PASTAR_OK;
-}
-
-int RcclTransport::exchange_counts(pastar_ctx *c, const unsigned long long *send, unsigned long long *recv)
-{
-    const int G = c->n_shards;
-    HIP_TRY(hipMemcpyAsync(c->xcounts.p, send, 8 * G, hipMemcpyHostToDevice, c->stream));
-    NCCL_TRY(ncclGroupStart());
-    for (int d = 0; d < G; d++) {
-        NCCL_TRY(ncclSend(c->xcounts.p + d, 1, ncclUint64, d, comm_, c->stream));
-        NCCL_TRY(ncclRecv(c->xcounts.p + G + d, 1, ncclUint64, d, comm_, c->stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    HIP_TRY(hipMemcpyAsync(recv, c->xcounts.p + G, 8 * G, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memcpy(all, h, sizeof(int64_t) * count * G);
     return PASTAR_OK;
 }
 
@@ -1570,6 +1553,14 @@ int RcclTransport::broadcast(pastar_ctx *c, void *dev, size_t bytes, int root)
 {
     NCCL_TRY(ncclBroadcast(dev, dev, bytes, ncclUint8, root, comm_, c->stream));
     return PASTAR_OK;
+}
+
+int LocalTransport::gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all)
+{
+    int64_t *h = reinterpret_cast<int64_t *>(c->h_gather);
+    HIP_TRY(hipMemcpyAsync(h, dev_mine, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return allgather(h, count, all);
 }
 
 int LocalTransport::exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
@@ -1641,6 +1632,7 @@ int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group 
     c->hp.shard = shard_rank;
     HIP_TRY(hipMemcpy(c->dP.p, &c->hp, sizeof(c->hp), hipMemcpyHostToDevice));
     if (group->G > 1) {
+        PA_TRY(c->xred.alloc((size_t)(group->G + 1) * kGatherMax));
         c->tr.reset(new LocalTransport(group, shard_rank));
         group->members++;
         for (int d = 0; d < 8; d++) {  // peer access for the copies, where the link allows it
