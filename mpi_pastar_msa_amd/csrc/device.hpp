@@ -316,13 +316,55 @@ __device__ __forceinline__ int64_t lookup(const uint64_t *__restrict__ table, ui
     return -1;
 }
 
+// The DevProblem fields the per-level code of the search kernel reads (key
+// packing, lengths, goal, gap costs, shard partition), copied into registers
+// once at kernel start.  Read through the DevProblem reference inside the
+// level loop, each would be a vector load the compiler cannot hoist past the
+// loop's table writes (it cannot prove they do not alias), i.e. a chain of
+// dependent global round trips on every level.  Same field names as
+// DevProblem, so the helpers take either.
+template <int N, int KW>
+struct KConst {
+    static constexpr int NMAX = N ? N : kMaxN;
+    int len[NMAX], kword[NMAX], kshift[NMAX], kbits[NMAX];
+    uint64_t goal_key[KW];
+    int gap_open, gap_ext, gap_gap;
+    int hash_type, hash_shift, n_shards, shard;
+    const int2 *HC;
+};
+
+template <int N, int KW>
+__device__ __forceinline__ KConst<N, KW> load_kconst(const DevProblem &P)
+{
+    KConst<N, KW> k;
+#pragma unroll
+    for (int i = 0; i < KConst<N, KW>::NMAX; i++) {
+        k.len[i] = P.len[i];
+        k.kword[i] = P.kword[i];
+        k.kshift[i] = P.kshift[i];
+        k.kbits[i] = P.kbits[i];
+    }
+#pragma unroll
+    for (int w = 0; w < KW; w++)
+        k.goal_key[w] = P.goal_key[w];
+    k.gap_open = P.gap_open;
+    k.gap_ext = P.gap_ext;
+    k.gap_gap = P.gap_gap;
+    k.hash_type = P.hash_type;
+    k.hash_shift = P.hash_shift;
+    k.n_shards = P.n_shards;
+    k.shard = P.shard;
+    k.HC = P.HC;
+    return k;
+}
+
 // ---------------------------------------------------------------------------
 // CoordHash owner (CoordHash.cpp:107-245) on device, for the shard partition.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int ilog2_floor(int v) { return 31 - __clz(v); }
 
-template <int NMAX>
-__device__ __forceinline__ int owner_dev(const DevProblem &P, int n, const int (&pos)[NMAX], int size)
+template <int NMAX, typename PP>
+__device__ __forceinline__ int owner_dev(const PP &P, int n, const int (&pos)[NMAX], int size)
 {
     if (size <= 1)
         return 0;
@@ -376,8 +418,8 @@ struct Parent {
     int g, pmask, blocked;
 };
 
-template <int N, int KW>
-__device__ __forceinline__ void decode_key(const DevProblem &P, int n, const uint64_t (&key)[KW],
+template <int N, int KW, typename PP>
+__device__ __forceinline__ void decode_key(const PP &P, int n, const uint64_t (&key)[KW],
                                            int (&pos)[Parent<N, KW>::NMAX])
 {
 #pragma unroll
@@ -399,8 +441,8 @@ __device__ __forceinline__ void decode_key(const DevProblem &P, int n, const uin
 // Fills terms[q], q = p*4 + c, for q in [glane, 4P) step lpn: one HC
 // gather per term (the c = 3 term also reads the substitution cost of the
 // parent's cell).
-template <int N, int KW>
-__device__ __forceinline__ void stage_terms(const DevProblem &P, int n, int npairs, const PairConst *pc,
+template <int N, int KW, typename PP>
+__device__ __forceinline__ void stage_terms(const PP &P, int n, int npairs, const PairConst *pc,
                                             const Parent<N, KW> &par, int2 *terms, int glane, int lpn)
 {
     for (int q = glane; q < 4 * npairs; q += lpn) {
@@ -436,6 +478,60 @@ __device__ __forceinline__ void stage_terms(const DevProblem &P, int n, int npai
     }
 }
 
+// stage_terms for a fixed N: the gathers of a lane's terms (a compile-time
+// count) are all issued before the first is waited for, one memory round
+// trip per parent instead of one per term.
+template <int N, int KW, typename PP>
+__device__ __forceinline__ void stage_terms_fixed(const PP &P, const PairConst *pc, const Parent<N, KW> &par,
+                                                  int2 *terms, int glane)
+{
+    static_assert(N > 0, "fixed N only");
+    constexpr int NP = N * (N - 1) / 2;
+    constexpr int LPN = (1 << N) < 64 ? (1 << N) : 64;
+    constexpr int NT = (4 * NP + LPN - 1) / LPN;
+    int hv[NT], gv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const int q = glane + t * LPN;
+        hv[t] = 0;
+        gv[t] = 0;
+        if (q < 4 * NP) {
+            const int p = q >> 2, c = q & 3;
+            const PairConst k = pc[p];
+            int px = 0, py = 0;
+#pragma unroll
+            for (int i = 0; i < N; i++) {
+                if (i == k.x)
+                    px = par.pos[i];
+                if (i == k.y)
+                    py = par.pos[i];
+            }
+            const int bx = c >> 1, by = c & 1;
+            const int2 *cells = P.HC + k.off;
+            if (px + bx <= k.lx && py + by <= k.ly)
+                hv[t] = cells[(int64_t)(px + bx) * k.row + (py + by)].x;
+            if (c == 3) {
+                gv[t] = cells[(int64_t)px * k.row + py].y;
+            } else {
+                int g0;
+                if (c == 2)  // x moves, y idle: open iff y moved into the parent
+                    g0 = ((par.pmask >> k.y) & 1) ? P.gap_open : P.gap_ext;
+                else if (c == 1)
+                    g0 = ((par.pmask >> k.x) & 1) ? P.gap_open : P.gap_ext;
+                else
+                    g0 = P.gap_gap;
+                gv[t] = g0 * k.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const int q = glane + t * LPN;
+        if (q < 4 * NP)
+            terms[q] = make_int2(gv[t], hv[t]);
+    }
+}
+
 // Sum of the staged terms for neighbour mask m: (delta g, h).
 template <int N>
 __device__ __forceinline__ int2 child_cost(const DevProblem &P, int npairs, const int2 *terms, int m)
@@ -465,8 +561,8 @@ __device__ __forceinline__ int2 child_cost(const DevProblem &P, int npairs, cons
     return make_int2(dg, hh);
 }
 
-template <int N, int KW>
-__device__ __forceinline__ void child_key(const DevProblem &P, int n, const uint64_t (&key)[KW], int m,
+template <int N, int KW, typename PP>
+__device__ __forceinline__ void child_key(const PP &P, int n, const uint64_t (&key)[KW], int m,
                                           uint64_t (&out)[KW])
 {
 #pragma unroll

@@ -529,8 +529,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
 // All lanes of the wave must call it.
-template <int KW>
-__device__ __forceinline__ void route_child(const SearchArgs &a, const DevProblem &P, StepStats *st, int f0, int w,
+template <int KW, typename PP>
+__device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned long long &claimed, unsigned long long &ovf,
                                             const LocalPush<KW> &lp, bool remote_in = false, bool has_pre = false,
@@ -922,8 +922,10 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     // and 1- or 2-word keys
     constexpr bool kPf = N > 0 && KW <= 2;
     Ctl *ctl = a.ctl;
-    const DevProblem &P = *a.P;
-    const int n = N ? N : P.n;
+    const DevProblem &Pg = *a.P;
+    // the fields the level loop reads, in registers (KConst)
+    const KConst<N, KW> P = load_kconst<N, KW>(Pg);
+    const int n = N ? N : Pg.n;
     const int lpn = (1 << n) < 64 ? (1 << n) : 64;
     const int npw = 64 / lpn;
     const int per_block = kWaves * npw;
@@ -941,7 +943,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const bool timing = (view.timing & 1) && nb;
     if (timing && blockIdx.x < kArrive && threadIdx.x == 0)
         __hip_atomic_store(&a.stamps[blockIdx.x], device_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int npairs = P.npairs;
+    const int npairs = N ? N * (N - 1) / 2 : Pg.npairs;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
         if (r < kRanges)
             bstart[r] = ctl->b_start[r];
     }
-    stage_pairs(P, pc);
+    stage_pairs(Pg, pc);
     const bool bprof = (view.timing & 4) && timing && blockIdx.x == 0 && threadIdx.x == 0;
     unsigned long long bt0 = bprof ? device_clock() : 0, bt;
 #define BPHASE(k)                                     \
@@ -1045,8 +1047,12 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
                     has_pf = true;
                 }
             }
-            stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
+            if constexpr (N > 0)
+                stage_terms_fixed<N, KW>(P, pc, par_, terms, glane);
+            else
+                stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
         }
+        BPHASE(6)
         if (local) {  // uniform: a whole level is local or not
             // current iff nobody has improved the node since it was queued
             // (a larger or unset best is this block's own update, not yet
@@ -1077,7 +1083,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             for (int k = 0; k < KW; k++)
                 ck[k] = 0;
             if (valid) {
-                const int2 dc = child_cost<N>(P, npairs, terms, m);
+                const int2 dc = child_cost<N>(Pg, npairs, terms, m);
                 g = par_.g + dc.x;
                 h = dc.y;
                 generated++;
@@ -1097,6 +1103,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp, false,
                             has_pf && r == 0, pf.w0, pf.w1, pf.w2);
         }
+        BPHASE(7)
         lds_barrier();
         BPHASE(3)
     };

@@ -1260,7 +1260,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         for (int k = 0; k < 4; k++)
             std::fprintf(stderr, " %.2f", (double)h.phase_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.timed_launches));
         std::fprintf(stderr, "\n[pastar] expand phases of block 0 (us/launch):");
-        for (int k = 0; k < 6; k++)
+        for (int k = 0; k < 8; k++)
             std::fprintf(stderr, " %.2f", (double)h.body_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.body_launches));
         std::fprintf(stderr, "\n");
     }

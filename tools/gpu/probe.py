@@ -17,7 +17,9 @@ for name in names:
     eng = Engine(Sequences.from_fasta(os.path.join(ROOT, "tests", "golden", name + ".fasta")))
     for d in depths:
         for i in range(reps):
-            r = eng.pa_star(PAStarOpt(profile=True, depth=d, verbose=verbose and i == reps - 1))
+            r = eng.pa_star(PAStarOpt(profile=True, depth=d, verbose=verbose and i == reps - 1,
+                                      table_slots_log2=int(os.environ.get("TABLE_LOG2", "0")),
+                                      pool_entries=int(os.environ.get("POOL", "0"))))
             ok = "ok" if r.score == KNOWN.get(name, r.score) else "WRONG"
             print("%-12s depth %d score %d %s exp %d steps %d wall %.2f ms expand %.1f us/launch select %.1f gap %.1f "
                   "retries %d" % (name, d, r.score, ok, r.expansions, r.steps, r.seconds * 1e3,
