@@ -481,54 +481,55 @@ __device__ __forceinline__ void stage_terms(const PP &P, int n, int npairs, cons
 // stage_terms for a fixed N: the gathers of a lane's terms (a compile-time
 // count) are all issued before the first is waited for, one memory round
 // trip per parent instead of one per term.
-template <int N, int KW, typename PP>
+template <int N, int KW, typename PP, typename F>
 __device__ __forceinline__ void stage_terms_fixed(const PP &P, const PairConst *pc, const Parent<N, KW> &par,
-                                                  int2 *terms, int glane)
+                                                  int2 *terms, int glane, F &&after_issue)
 {
     static_assert(N > 0, "fixed N only");
     constexpr int NP = N * (N - 1) / 2;
     constexpr int LPN = (1 << N) < 64 ? (1 << N) : 64;
     constexpr int NT = (4 * NP + LPN - 1) / LPN;
-    int hv[NT], gv[NT];
+    // branch-free: every address is clamped into its table (a term past 4P
+    // reads pair 0's cell and is dropped), so the compiler issues all 2*NT
+    // gathers back to back and waits once
+    int hraw[NT], graw[NT], g0w[NT];
+    bool hin[NT], mm[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) {
-        const int q = glane + t * LPN;
-        hv[t] = 0;
-        gv[t] = 0;
-        if (q < 4 * NP) {
-            const int p = q >> 2, c = q & 3;
-            const PairConst k = pc[p];
-            int px = 0, py = 0;
+        const int q0 = glane + t * LPN;
+        const int q = q0 < 4 * NP ? q0 : 0;
+        const int p = q >> 2, c = q & 3;
+        const PairConst k = pc[p];
+        int px = 0, py = 0;
 #pragma unroll
-            for (int i = 0; i < N; i++) {
-                if (i == k.x)
-                    px = par.pos[i];
-                if (i == k.y)
-                    py = par.pos[i];
-            }
-            const int bx = c >> 1, by = c & 1;
-            const int2 *cells = P.HC + k.off;
-            if (px + bx <= k.lx && py + by <= k.ly)
-                hv[t] = cells[(int64_t)(px + bx) * k.row + (py + by)].x;
-            if (c == 3) {
-                gv[t] = cells[(int64_t)px * k.row + py].y;
-            } else {
-                int g0;
-                if (c == 2)  // x moves, y idle: open iff y moved into the parent
-                    g0 = ((par.pmask >> k.y) & 1) ? P.gap_open : P.gap_ext;
-                else if (c == 1)
-                    g0 = ((par.pmask >> k.x) & 1) ? P.gap_open : P.gap_ext;
-                else
-                    g0 = P.gap_gap;
-                gv[t] = g0 * k.w;
-            }
+        for (int i = 0; i < N; i++) {
+            if (i == k.x)
+                px = par.pos[i];
+            if (i == k.y)
+                py = par.pos[i];
         }
+        const int bx = c >> 1, by = c & 1;
+        // global address space: a generic pointer would make these flat
+        // loads, which also count on the LDS counter (the pc reads of the
+        // next term would then wait for them)
+        const __attribute__((address_space(1))) int2 *cells =
+            (const __attribute__((address_space(1))) int2 *)(P.HC + k.off);
+        hin[t] = px + bx <= k.lx && py + by <= k.ly;
+        const int ix = px + bx <= k.lx ? px + bx : k.lx, iy = py + by <= k.ly ? py + by : k.ly;
+        hraw[t] = cells[(int64_t)ix * k.row + iy].x;
+        graw[t] = cells[(int64_t)px * k.row + py].y;
+        mm[t] = c == 3;
+        // c = 2: x moves, y idle: gap open iff y moved into the parent
+        const int g0 = c == 2 ? (((par.pmask >> k.y) & 1) ? P.gap_open : P.gap_ext)
+                              : (c == 1 ? (((par.pmask >> k.x) & 1) ? P.gap_open : P.gap_ext) : P.gap_gap);
+        g0w[t] = g0 * k.w;
     }
+    after_issue();  // more loads the caller overlaps with the gathers
 #pragma unroll
     for (int t = 0; t < NT; t++) {
         const int q = glane + t * LPN;
         if (q < 4 * NP)
-            terms[q] = make_int2(gv[t], hv[t]);
+            terms[q] = make_int2(mm[t] ? graw[t] : g0w[t], hin[t] ? hraw[t] : 0);
     }
 }
 

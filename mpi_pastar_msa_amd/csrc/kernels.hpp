@@ -1038,19 +1038,25 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
             for (int i = 0; i < Parent<N, KW>::NMAX; i++)
                 if ((N || i < n) && par_.pos[i] >= P.len[i])
                     par_.blocked |= 1 << i;
-            if constexpr (kPf) {
-                const int m = glane;
-                if (m >= 1 && m < masks && !(m & par_.blocked)) {
+            // the slot prefetch is issued right after the gathers (before
+            // their wait), so waiting for the gathers never waits for it
+            auto prefetch = [&] {
+                if constexpr (kPf) {
+                    // issued by every lane (the slot index is masked into
+                    // the table), so the wait counts do not depend on it
+                    const int m = glane;
                     uint64_t ck[KW];
                     child_key<N, KW>(P, n, par_.key, m, ck);
                     pf = slot_prefetch<KW>(a.table, a.cap_mask, ck);
-                    has_pf = true;
+                    has_pf = m >= 1 && m < masks && !(m & par_.blocked);
                 }
-            }
-            if constexpr (N > 0)
-                stage_terms_fixed<N, KW>(P, pc, par_, terms, glane);
-            else
+            };
+            if constexpr (N > 0) {
+                stage_terms_fixed<N, KW>(P, pc, par_, terms, glane, prefetch);
+            } else {
+                prefetch();
                 stage_terms<N, KW>(P, n, npairs, pc, par_, terms, glane, lpn);
+            }
         }
         BPHASE(6)
         if (local) {  // uniform: a whole level is local or not
