@@ -944,9 +944,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     hc.max_steps = cfg.max_steps;
     hc.k_start = ~0ull;
     hc.timing = 0;
-    if (cfg.profile) {  // bits: 1 expand launch timing, 2 select phases, 4 expand phases (diagnostics)
+    if (cfg.profile) {  // bits: 1 expand launch timing (default), 2 select phases, 4 expand phases (diagnostics, PASTAR_TIMING_MASK=7)
         const char *e = std::getenv("PASTAR_TIMING_MASK");
-        hc.timing = e && *e ? std::atoi(e) : 7;
+        hc.timing = e && *e ? std::atoi(e) : 1;
     }
     hc.fuse = G == 1 ? 1 : 0;  // one shard: select runs in the tail of expand
     hc.depth = cfg.depth;

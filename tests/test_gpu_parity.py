@@ -189,3 +189,62 @@ def test_sharded_search_repeated_exact(shards, depth, profile, kat):
     for _ in range(4):
         res, rows = sharded_search(seqs, shards, opt=PAStarOpt(depth=depth, profile=profile))
         assert [r.score for r in res] == [ref["score"]] * shards
+
+
+@pytest.mark.parametrize("hash_type,shift,shards", [("FSUM", 12, 3), ("PZORDER", 8, 4), ("PSUM", 4, 2),
+                                                    ("FZORDER", 0, 4), ("FZORDER", 21, 2)])
+def test_sharded_search_every_partition_hash(hash_type, shift, shards, kat, oracles):
+    """The alternate CoordHash partitions (CoordHash.cpp:28-166) and the shift
+    range ends (:241) route the same search: optimal score and a valid
+    optimal alignment for every owner function."""
+    from mpi_pastar_msa_amd import sharded_search
+    ref = kat["inputs"]["syn4x200_s1"]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    res, rows = sharded_search(seqs, shards, opt=PAStarOpt(batch_nodes=4096), hash_type=hash_type,
+                               hash_shift=shift)
+    assert [r.score for r in res] == [ref["score"]] * shards
+    assert oracles["syn4x200_s1"].alignment_cost(rows) == ref["score"]
+
+
+def _cli(*args):
+    import os
+    import subprocess
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi_pastar_msa_amd", "bin",
+                       "msa_pastar")
+    return subprocess.run([cli, *args], capture_output=True, text=True, timeout=120)
+
+
+@pytest.mark.parametrize("name", ["PF08184", "test2", "kinase"])
+def test_cli_output_matches_reference_format(name, kat, oracles):
+    """msa_pastar end to end on the GPU: the reference's output lines
+    (Node.cpp:41-47 final score, backtrace.cpp:136-191 similarity and rows,
+    PAStar.cpp:591-619 node-count table) with the reference's values."""
+    ref = kat["inputs"][name]
+    r = _cli(golden(ref["file"]))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    o = oracles[name]
+    ends = " ".join(str(L) for L in o.lengths)
+    score = ref["score"]
+    assert "Final Score: (%s)\tg - %d (h - 0 f - %d)" % (ends, score, score) in lines
+    assert lines[0] == "Starting pairwise alignments... done!"
+    assert any(l.startswith("Running PAStar with: 1 threads") and "Full-Zorder hash, 12 shift." in l for l in lines)
+    sim = [l for l in lines if l.startswith("Similarity: ")]
+    assert len(sim) == 1
+    i = lines.index(sim[0])
+    rows = lines[i + 2:i + 2 + len(o.lengths)]
+    assert o.alignment_cost(rows) == score
+    if "alignment_md5" in ref:
+        assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+    if "similarity" in ref:
+        assert sim[0] == "Similarity: %s%%" % ref["similarity"]
+    assert lines[i + 2 + len(o.lengths)] == "Total nodes count:"
+    assert lines[-1].startswith("Sum\tOpenList:")
+
+
+def test_cli_hash_options():
+    """-y / -s reach the engine and are echoed like the reference does."""
+    r = _cli("-y", "PSUM", "-s", "5", golden("test2.fasta"))
+    assert r.returncode == 0, r.stderr
+    assert any("Partial-Sum hash, 5 shift." in l for l in r.stdout.splitlines()), r.stdout
+    assert "g - 45037 (h - 0 f - 45037)" in r.stdout
