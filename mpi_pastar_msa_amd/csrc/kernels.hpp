@@ -1449,20 +1449,25 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
                             const uint64_t *__restrict__ start, int max, int local_only,
                             int32_t *__restrict__ masks, uint64_t *__restrict__ last_key, int *__restrict__ info)
 {
-    const DevProblem &P = *Pp;
-    const int n = N ? N : P.n;
+    const DevProblem &Pg = *Pp;
+    const int n = N ? N : Pg.n;
     constexpr int SW = slot_words<KW>();
-    uint64_t key[KW];
+    // one dependent chain: the constants in registers up front, and each
+    // step's probe reads a slot's key words and best in one go
+    const KConst<N, KW> P = load_kconst<N, KW>(Pg);
+    uint64_t origin[KW], key[KW];
 #pragma unroll
-    for (int w = 0; w < KW; w++)
+    for (int w = 0; w < KW; w++) {
+        origin[w] = Pg.origin_key[w];
         key[w] = start[w];
+    }
     int steps = 0, status = 0;
     for (;;) {
-        bool origin = true;
+        bool at_origin = true;
 #pragma unroll
         for (int w = 0; w < KW; w++)
-            origin &= key[w] == P.origin_key[w];
-        if (origin) {
+            at_origin &= key[w] == origin[w];
+        if (at_origin) {
             status = 1;
             break;
         }
@@ -1470,12 +1475,49 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
             status = 2;
             break;
         }
-        const int64_t s = lookup<KW>(table, cap_mask, key);
-        if (s < 0) {
+        // lookup (backtrace.cpp:47-69 ClosedList find), slot words
+        // [0, KW] = key + best in one read
+        uint64_t idx = key_hash<KW>(key) & cap_mask;
+        int m = -1;
+        for (int probe = 0; probe < kMaxProbe; probe++) {
+            // the slot's key words and best in one round trip (plain loads
+            // get best sunk behind the key compare, a second trip per step)
+            const uint64_t *sl = table + idx * SW;
+            uint64_t wv[KW + 1];
+            if constexpr (KW <= 2) {
+                typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                u64x2 a0, a1;
+                asm volatile("global_load_dwordx4 %0, %2, off\n\t"
+                             "global_load_dwordx4 %1, %2, off offset:16\n\t"
+                             "s_waitcnt vmcnt(0)"
+                             : "=&v"(a0), "=&v"(a1)
+                             : "v"(sl)
+                             : "memory");
+                wv[0] = a0.x;
+                wv[1] = a0.y;
+                if constexpr (KW == 2)
+                    wv[2] = a1.x;
+            } else {
+#pragma unroll
+                for (int w = 0; w <= KW; w++)
+                    wv[w] = sl[w];
+            }
+            if (wv[0] == 0)
+                break;
+            bool same = true;
+#pragma unroll
+            for (int w = 0; w < KW; w++)
+                same &= wv[w] == key[w];
+            if (same) {
+                m = (int)(uint32_t)wv[KW];
+                break;
+            }
+            idx = (idx + 1) & cap_mask;
+        }
+        if (m < 0) {
             status = -1;
             break;
         }
-        const int m = (int)(uint32_t)table[(uint64_t)s * SW + KW];
         masks[steps++] = m;
         int pos[Parent<N, KW>::NMAX];
         decode_key<N, KW>(P, n, key, pos);
