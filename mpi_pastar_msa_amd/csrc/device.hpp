@@ -25,7 +25,13 @@ constexpr int kMaxN = 16;
 constexpr int kMaxPairs = kMaxN * (kMaxN - 1) / 2;
 constexpr int kBlock = 256;           // threads per block (4 waves)
 constexpr int kWaves = kBlock / 64;
-constexpr int kTPerWave = 512;        // int2 pair-corner terms per wave (LDS)
+constexpr int kTPerWave = 512;        // int2 pair-corner terms per wave (LDS), any N <= kMaxN
+// terms one wave stages for a fixed N: 64 / min(2^N, 64) parents x 4P
+// (<= 112 for N <= 8), so the search kernel's LDS allows 4+ blocks per CU
+__host__ __device__ constexpr int terms_per_wave(int n)
+{
+    return n == 0 ? kTPerWave : (64 / ((1 << n) < 64 ? (1 << n) : 64)) * 4 * (n * (n - 1) / 2);
+}
 constexpr uint64_t kMark = 1ull << 63;  // key word written / occupied
 constexpr int kMaxProbe = 1 << 16;
 constexpr int kIntMax = 0x7fffffff;

@@ -915,7 +915,7 @@ __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const SelView 
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
 // (PAStar::enqueue + conditional_enqueue, :219-237).
 template <int N, int KW>
-__global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
     // child-slot prefetch: fixed N (the rounds of 64 children are static)
@@ -947,7 +947,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(SearchArgs a)
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
-    __shared__ int2 terms_all[kWaves][kTPerWave];
+    __shared__ int2 terms_all[kWaves][terms_per_wave(N)];
     __shared__ unsigned long long prefix[kRanges + 1], bstart[kRanges];
     __shared__ PairConst pc[kMaxPairs];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
