@@ -59,11 +59,22 @@ __host__ __device__ constexpr size_t pairalign_lds_bytes(int maxl2, int alpha, b
 
 // SUB_LDS: the distance table is staged in LDS (every read in the sweep is
 // then an LDS read, and the per-step waits never include the stores).
-template <bool SUB_LDS>
+// WRITE_H: also store the plain table H (only pastar_gpu_pair_table reads it;
+// the search and h read HC).
+//
+// Stores: a lane owns one row, so a per-step store touches 64 rows (64 cache
+// lines) for 4-8 B each and the CU's address path, not HBM, bounds the sweep.
+// The HC cells of kPaChunk consecutive steps are therefore kept in registers
+// and stored as one run of kPaChunk * 8 B per lane (16-B vector stores).
+constexpr int kPaChunk = 8;
+typedef int pa_v4i __attribute__((ext_vector_type(4), aligned(8)));
+
+template <bool SUB_LDS, bool WRITE_H>
 __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const DevProblem *__restrict__ Pp,
                                                                        int32_t *__restrict__ H,
                                                                        int2 *__restrict__ HC)
 {
+    static_assert(kPaChunk == 8, "the progress handshake runs every 8 steps, once per chunk");
     const DevProblem &P = *Pp;
     const int p = blockIdx.x;
     const int lane = lane_id(), wave = threadIdx.x >> 6;
@@ -118,54 +129,102 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
         int j = L2 + 63 - lane;         // column of step t: L2 - (t - (63 - lane))
         int cost = (j >= 0 && j <= L2) ? crow[s2[j]] : 0;  // one step ahead
         const int nsteps = L2 + 64;
-        for (int t = 0; t < nsteps; t++, j--) {
-            if (band > 0 && t <= L2 && (t & 7) == 0) {
+        for (int t0 = 0; t0 < nsteps; t0 += kPaChunk) {
+            if (band > 0 && t0 <= L2) {
                 // lane 63 reads column L2 - t of band - 1's top row, written
                 // by its lane 0 at its step t + 63; one check covers 8 steps
-                const int need = ((band - 1) << 16) | (t + 71 < nsteps ? t + 71 : nsteps);
+                const int need = ((band - 1) << 16) | (t0 + 71 < nsteps ? t0 + 71 : nsteps);
                 while (*prev_progress < need)
                     __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");  // the row reads below stay after the wait
             }
-            // row i + 1 at column j: produced last step by the lane above
-            // (lane 63: the previous band's top row); (i + 1, j + 1) is last
-            // step's (i + 1, j).  Branch-free: every lane computes, only
-            // cells inside the table are stored.
-            const bool in = row_ok && j >= 0 && j <= L2;
-            const int jc = j < 0 ? 0 : (j > L2 ? L2 : j);
-            const int m_up = from_lane_above(m), a_up = from_lane_above(a);
-            const int lb = below[jc], lbd = belowd[jc];
-            diag = down;
-            down = use_lds_below ? lb : m_up;
-            adown = use_lds_below ? lbd : a_up;
-            const int cost_here = cost;
-            const int jn = j - 1 < 0 ? 0 : (j - 1 > L2 ? L2 : j - 1);
-            cost = crow[s2[jn]];
-            const int right = m, aright = a;
-            const int c0 = down + (adown == kGapX ? GE : GO);
-            const int c1 = right + (aright == kGapY ? GE : GO);
-            int mm = c0 < c1 ? c0 : c1;
-            int aa = c0 < c1 ? kGapX : kGapY;
-            const int c2 = diag + cost_here;
-            aa = c2 < mm ? kNoGap : aa;
-            mm = c2 < mm ? c2 : mm;
-            const bool last_col = j == L2;
-            // borders (PairAlign.cpp:142-160)
-            const int m_lastcol = row_above_last ? GO : down + GE;
-            const int m_lastrow = (j == L2 - 1) ? GO : right + GE;
-            mm = last_row ? (last_col ? 0 : m_lastrow) : (last_col ? m_lastcol : mm);
-            aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
-            if (in) {
-                m = mm;
-                a = aa;
-                Mrow[j] = mm;
-                Crow[j] = make_int2(mm * wgt, cost_here * wgt);
-                if (lane == 0) {
-                    top[j] = mm;
-                    topd[j] = (uint8_t)aa;
+            const int j0 = j;  // this lane's column at step t0
+            // the chunk's LDS operands, issued together ahead of the DP chain
+            // (one LDS round trip per chunk, not two per step): the previous
+            // band's top row (lane 63) and the distance row for columns
+            // j0 - 1 .. j0 - 8 (the cost of step u + 1)
+            int lb[kPaChunk], lbd[kPaChunk], nc[kPaChunk];
+#pragma unroll
+            for (int u = 0; u < kPaChunk; u++) {
+                const int jj = j0 - u;
+                const int jc = jj < 0 ? 0 : (jj > L2 ? L2 : jj);
+                const int jn = jj - 1 < 0 ? 0 : (jj - 1 > L2 ? L2 : jj - 1);
+                lb[u] = below[jc];
+                lbd[u] = belowd[jc];
+                nc[u] = s2[jn];
+            }
+#pragma unroll
+            for (int u = 0; u < kPaChunk; u++)
+                nc[u] = crow[nc[u]];
+            int2 cb[kPaChunk];
+            int tb[kPaChunk], tbd[kPaChunk];
+#pragma unroll
+            for (int u = 0; u < kPaChunk; u++, j--) {
+                // row i + 1 at column j: produced last step by the lane above
+                // (lane 63: the previous band's top row); (i + 1, j + 1) is
+                // last step's (i + 1, j).  Branch-free: every lane computes,
+                // only cells inside the table are kept.  Steps past the sweep
+                // (t >= nsteps) have j < 0 on every lane and change nothing.
+                const bool in = row_ok && j >= 0 && j <= L2;
+                const int m_up = from_lane_above(m), a_up = from_lane_above(a);
+                diag = down;
+                down = use_lds_below ? lb[u] : m_up;
+                adown = use_lds_below ? lbd[u] : a_up;
+                const int cost_here = cost;
+                cost = nc[u];
+                const int right = m, aright = a;
+                const int c0 = down + (adown == kGapX ? GE : GO);
+                const int c1 = right + (aright == kGapY ? GE : GO);
+                int mm = c0 < c1 ? c0 : c1;
+                int aa = c0 < c1 ? kGapX : kGapY;
+                const int c2 = diag + cost_here;
+                aa = c2 < mm ? kNoGap : aa;
+                mm = c2 < mm ? c2 : mm;
+                const bool last_col = j == L2;
+                // borders (PairAlign.cpp:142-160)
+                const int m_lastcol = row_above_last ? GO : down + GE;
+                const int m_lastrow = (j == L2 - 1) ? GO : right + GE;
+                mm = last_row ? (last_col ? 0 : m_lastrow) : (last_col ? m_lastcol : mm);
+                aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
+                cb[u] = make_int2(mm * wgt, cost_here * wgt);
+                m = in ? mm : m;
+                a = in ? aa : a;
+                tb[u] = m;
+                tbd[u] = a;
+                if constexpr (WRITE_H)
+                    if (in)
+                        Mrow[j] = mm;
+            }
+            // lane 0's cells are the band's top row, which the next band
+            // reads: stored once per chunk, then the chunk is published
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < kPaChunk; u++) {
+                    const int jj = j0 - u;
+                    if (row_ok && jj >= 0 && jj <= L2) {
+                        top[jj] = tb[u];
+                        topd[jj] = (uint8_t)tbd[u];
+                    }
+                }
+                *my_progress = (band << 16) | (t0 + kPaChunk < nsteps ? t0 + kPaChunk : nsteps);
+            }
+            // the chunk's cells of this lane's row are columns j0 - 7 .. j0
+            const int jlo = j0 - (kPaChunk - 1);
+            if (row_ok && jlo >= 0 && j0 <= L2) {
+                pa_v4i *dst = reinterpret_cast<pa_v4i *>(Crow + jlo);
+#pragma unroll
+                for (int k = 0; k < kPaChunk / 2; k++) {
+                    const int2 lo = cb[kPaChunk - 1 - 2 * k], hi = cb[kPaChunk - 2 - 2 * k];
+                    dst[k] = pa_v4i{lo.x, lo.y, hi.x, hi.y};
+                }
+            } else if (row_ok) {
+#pragma unroll
+                for (int u = 0; u < kPaChunk; u++) {
+                    const int jj = j0 - u;
+                    if (jj >= 0 && jj <= L2)
+                        Crow[jj] = cb[u];
                 }
             }
-            if (lane == 0 && ((t & 7) == 7 || t == nsteps - 1))
-                *my_progress = (band << 16) | (t + 1);  // after this step's top-row write
         }
     }
 }
@@ -182,7 +241,7 @@ __global__ void h_kernel(const DevProblem *__restrict__ Pp, const uint16_t *__re
     int h = 0;
     for (int p = 0; p < P.npairs; p++) {
         const int x = P.pair_x[p], y = P.pair_y[p];
-        h += P.H[P.h_off[p] + (int64_t)c[x] * P.h_row[p] + c[y]] * P.weight[p];
+        h += P.HC[P.h_off[p] + (int64_t)c[x] * P.h_row[p] + c[y]].x;  // H * w
     }
     out[k] = h;
 }

@@ -259,6 +259,7 @@ struct pastar_ctx {
     DevBuf<uint8_t> dcodes;
     DevBuf<int32_t> dsub;
     bool heuristic_ready = false;
+    bool plain_h_ready = false;  // H written (pastar_gpu_pair_table)
 
     // search state
     DevBuf<uint64_t> table;
@@ -665,35 +666,42 @@ void pastar_gpu_destroy(pastar_ctx *c)
     delete c;
 }
 
+// One launch of the PairAlign wavefront (one workgroup per pair): LDS holds
+// the rows below the current bands, the codes of sequence y and, when it
+// fits, the distance table.  write_h also stores the plain tables H.
+static int launch_pairalign(pastar_ctx *c, bool write_h)
+{
+    int maxl2 = 0;
+    for (int k = 0; k < c->npairs; k++)
+        maxl2 = std::max(maxl2, c->hp.len[c->hp.pair_y[k]]);
+    const bool sub_lds = c->hp.alpha * c->hp.alpha * 4 <= 32 * 1024;
+    if (maxl2 >= 65536 - 64)
+        return fail(PASTAR_EINVAL, "sequence too long for the PairAlign kernel (%d)", maxl2);
+    const size_t lds = pairalign_lds_bytes(maxl2, c->hp.alpha, sub_lds);
+    if (lds > 160 * 1024)
+        return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl2);
+    const void *fn = sub_lds ? (write_h ? (const void *)pairalign_wave_kernel<true, true>
+                                        : (const void *)pairalign_wave_kernel<true, false>)
+                             : (write_h ? (const void *)pairalign_wave_kernel<false, true>
+                                        : (const void *)pairalign_wave_kernel<false, false>);
+    if (lds > 64 * 1024)
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p};
+    HIP_TRY(hipLaunchKernel(fn, dim3(c->npairs), dim3(64 * kPaWaves), args, lds, c->stream));
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return PASTAR_OK;
+}
+
 int pastar_gpu_build_heuristic(pastar_ctx *c)
 {
     if (!c)
         return fail(PASTAR_EINVAL, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
-    // one wavefront per pair (pairalign_wave_kernel): LDS holds the row
-    // below the current band, the codes of sequence y and, when it fits, the
-    // distance table
-    int maxl2 = 0;
-    for (int k = 0; k < c->npairs; k++)
-        maxl2 = std::max(maxl2, c->hp.len[c->hp.pair_y[k]]);
-    const int sub_lds = c->hp.alpha * c->hp.alpha * 4 <= 32 * 1024 ? 1 : 0;
-    if (maxl2 >= 65536 - 64)
-        return fail(PASTAR_EINVAL, "sequence too long for the PairAlign kernel (%d)", maxl2);
-    const size_t lds = pairalign_lds_bytes(maxl2, c->hp.alpha, sub_lds != 0);
-    if (lds > 160 * 1024)
-        return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl2);
-    const void *fn = sub_lds ? (const void *)pairalign_wave_kernel<true> : (const void *)pairalign_wave_kernel<false>;
-    if (lds > 64 * 1024)
-        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (sub_lds)
-        hipLaunchKernelGGL(pairalign_wave_kernel<true>, dim3(c->npairs), dim3(64 * kPaWaves), lds, c->stream, c->dP.p,
-                           c->dH.p, c->dHC.p);
-    else
-        hipLaunchKernelGGL(pairalign_wave_kernel<false>, dim3(c->npairs), dim3(64 * kPaWaves), lds, c->stream,
-                           c->dP.p, c->dH.p, c->dHC.p);
-    PA_TRY(check_launch());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the search and h read only HC; H is written on demand (pair_table)
+    PA_TRY(launch_pairalign(c, false));
     c->heuristic_ready = true;
+    c->plain_h_ready = false;
     return PASTAR_OK;
 }
 
@@ -704,6 +712,10 @@ int pastar_gpu_pair_table(pastar_ctx *c, int pair, int32_t *out)
     if (!c->heuristic_ready)
         return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
     HIP_TRY(hipSetDevice(c->device));
+    if (!c->plain_h_ready) {
+        PA_TRY(launch_pairalign(c, true));
+        c->plain_h_ready = true;
+    }
     const size_t cells = (size_t)(c->hp.len[c->hp.pair_x[pair]] + 1) * (c->hp.len[c->hp.pair_y[pair]] + 1);
     HIP_TRY(hipMemcpy(out, c->dH.p + c->hp.h_off[pair], cells * 4, hipMemcpyDeviceToHost));
     return PASTAR_OK;
