@@ -439,6 +439,10 @@ struct Queues {
 };
 
 constexpr int kMaxExpandBlocks = 4096;
+// register budget of expand_kernel<N, KW>: waves per SIMD it must fit, which
+// is also its resident blocks per CU (a block is one wave on each SIMD)
+// (5 for N <= 5 spills 36-72 B per lane and ran kinase 20% slower)
+__host__ __device__ constexpr int expand_waves_per_eu(int, int) { return 4; }
 constexpr int kTraceSteps = 4096;
 
 struct SearchArgs {
@@ -952,6 +956,27 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
     select_block(a, load_view(a.ctl));
 }
 
+// A batch parent's slot words: key, best, aux.
+template <int KW>
+struct PSlot {
+    uint64_t key[KW];
+    uint64_t best, aux;
+};
+
+template <int KW>
+__device__ __forceinline__ PSlot<KW> load_pslot(const uint64_t *__restrict__ table, uint32_t slot)
+{
+    constexpr int SW = slot_words<KW>();
+    const uint64_t *s = table + (uint64_t)slot * SW;
+    PSlot<KW> o;
+#pragma unroll
+    for (int k = 0; k < KW; k++)
+        o.key[k] = s[k];
+    o.best = s[KW];
+    o.aux = s[KW + 1];
+    return o;
+}
+
 // Entry i of the current batch (binary search over the range prefix in LDS).
 __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const SelView &v, const unsigned long long *prefix,
                                              const unsigned long long *bstart, unsigned long long i)
@@ -974,7 +999,7 @@ __device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const SelView 
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
 // (PAStar::enqueue + conditional_enqueue, :219-237).
 template <int N, int KW>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void expand_kernel(SearchArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_waves_per_eu(N, KW)))) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
     // child-slot prefetch: fixed N (the rounds of 64 children are static)
@@ -1037,7 +1062,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // thread of the block calls it (it holds a block barrier).
     // `local`: a continuation entry (parent fields carried in LDS); else a
     // batch entry {slot, f} whose parent is read from the table
-    auto process = [&](bool ok, const Entry e, const LEntry<KW> &le, bool local, const LocalPush<KW> &lp) {
+    auto process = [&](bool ok, const Entry e, const PSlot<KW> &ps, const LEntry<KW> &le, bool local,
+                       const LocalPush<KW> &lp) {
         Parent<N, KW> par_;
         par_.g = 0;
         par_.pmask = 0;
@@ -1059,12 +1085,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             lbest = s[KW];
             laux = s[KW + 1];
         } else if (ok) {
-            const uint64_t *s = a.table + (uint64_t)e.slot * SW;
+            // the slot words were loaded by the caller, a chunk ahead
 #pragma unroll
             for (int k = 0; k < KW; k++)
-                par_.key[k] = s[k];
-            const uint64_t best = s[KW];
-            const uint64_t aux = s[KW + 1];
+                par_.key[k] = ps.key[k];
+            const uint64_t best = ps.best;
+            const uint64_t aux = ps.aux;
             const int h = (int)(aux >> 32);
             par_.g = (int)(best >> 32);
             par_.pmask = (int)(uint32_t)best;
@@ -1198,13 +1224,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                            ? per_block * (int)rounds : kLocalCap;
     LocalPush<KW> lp{depth > 1 ? lq[0] : nullptr, &lq_count[0], f_limit, lq_cap, outq, &out_n};
     const LEntry<KW> no_le{};
+    // a block walks its chunks of the batch (grid-stride; the grid is about
+    // one resident wave of blocks) as a software pipeline: a chunk's parent
+    // slots and the next chunk's queue entries are loaded together, so a
+    // chunk waits for one memory round trip before staging, not three
+    // (entry: chunk table + pool, then the slot)
+    const PSlot<KW> no_ps{};
+    Entry e_nx{0, 0};
+    {
+        const unsigned long long node = (unsigned long long)blockIdx.x * per_block + wave * npw + group;
+        if (node < nb)
+            e_nx = batch_entry(a, view, prefix, bstart, node);
+    }
     for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
         const unsigned long long node = chunk * per_block + wave * npw + group;
         const bool ok = node < nb;
-        Entry e{0, 0};
+        const Entry e = e_nx;
+        PSlot<KW> ps = no_ps;
         if (ok)
-            e = batch_entry(a, view, prefix, bstart, node);
-        process(ok, e, no_le, false, lp);
+            ps = load_pslot<KW>(a.table, e.slot);
+        const unsigned long long nn = node + (unsigned long long)gridDim.x * per_block;
+        if (nn < nb)
+            e_nx = batch_entry(a, view, prefix, bstart, nn);
+        process(ok, e, ps, no_le, false, lp);
     }
     int cur = 0;
     for (int lvl = 1; lvl < depth; lvl++) {
@@ -1220,7 +1262,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int base = 0; base < cnt; base += per_block) {
             const int idx = base + wave * npw + group;
             const bool ok = idx < cnt;
-            process(ok, Entry{0, 0}, ok ? lq[cur][idx] : no_le, true, lq_next);
+            process(ok, Entry{0, 0}, no_ps, ok ? lq[cur][idx] : no_le, true, lq_next);
         }
         cur = nxt;
     }

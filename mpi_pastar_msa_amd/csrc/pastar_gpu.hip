@@ -1006,8 +1006,15 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.outbox_cap = cfg.outbox_cap;
 
     const dim3 blk(kBlock);
-    const dim3 expand_grid(
-        (unsigned)std::min<unsigned long long>(kMaxExpandBlocks, (cfg.kmax + per_block - 1) / per_block));
+    // about one resident wave of blocks: a block then walks several chunks
+    // of a large batch (pipelined) and pays its setup and final flush once
+    int n_cu = 256;
+    HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    unsigned long long max_blocks =
+        std::min<unsigned long long>(kMaxExpandBlocks, (unsigned long long)n_cu * expand_waves_per_eu(c->n, KW));
+    if (const char *e = std::getenv("PASTAR_EXPAND_BLOCKS"))  // tuning probe
+        max_blocks = std::max(1ull, std::strtoull(e, nullptr, 10));
+    const dim3 expand_grid((unsigned)std::min<unsigned long long>(max_blocks, (cfg.kmax + per_block - 1) / per_block));
 
     // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
     // its owner shard, through the same relax path as remote records
