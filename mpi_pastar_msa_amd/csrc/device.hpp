@@ -143,6 +143,25 @@ __host__ __device__ constexpr int slot_words()
     return KW <= 2 ? 4 : 8;
 }
 
+// Slots per 128-B cache line.  With 1-word keys a probe sequence starts at
+// the first slot of the line its hash falls in (then linear, across lines),
+// so the first probes of a key are one line: a prefetch of that line's key
+// words resolves most collisions without another memory round trip.  Longer
+// keys start at their hash slot: their prefetch covers one slot, and aligned
+// starts would only cluster the first probes (syn8x400 10% slower).
+template <int KW>
+__host__ __device__ constexpr int line_slots()
+{
+    return 128 / (slot_words<KW>() * 8);
+}
+
+template <int KW>
+__device__ __forceinline__ uint64_t probe_start(const uint64_t (&k)[KW], uint64_t cap_mask)
+{
+    const uint64_t h = key_hash<KW>(k) & cap_mask;
+    return KW == 1 ? h & ~(uint64_t)(line_slots<KW>() - 1) : h;
+}
+
 // Wave-aggregated append: one atomic per wave, lanes write compacted
 // (ballot + prefix popcount).  Must be reached by every lane of the wave.
 template <typename T>
@@ -181,30 +200,61 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
 // best only decreases, so a lagging read of it can only skip a relaxation
 // that would not improve anything.
 //
-// pre0..2 (KW <= 2, has_pre): the words of the first probe's slot, read by the caller
-// ahead of time (slot_prefetch); a read taken earlier can only lag more,
-// which the protocol already tolerates.
-template <int KW>
+// pre (has_pre): the key words and best of the first PFS slots of the probe
+// sequence, read by the caller ahead of time (slot_prefetch); a read taken
+// earlier can only lag more, which the protocol already tolerates (a slot
+// seen empty may have been claimed since: the CAS then fails and the slot is
+// re-read).
+template <int KW, int PFS>
+struct SlotWords {
+    uint64_t w[PFS][KW + 1];
+};
+
+template <int KW, int PFS>
 __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t cap_mask,
                                          const uint64_t (&key)[KW], int g, int pmask, int h,
-                                         bool &improved, bool &claimed, bool has_pre = false,
-                                         uint64_t pre0 = 0, uint64_t pre1 = 0, uint64_t pre2 = 0)
+                                         bool &improved, bool &claimed, bool has_pre,
+                                         const SlotWords<KW, PFS> &pre)
 {
     constexpr int SW = slot_words<KW>();
     improved = false;
     claimed = false;
-    uint64_t idx = key_hash<KW>(key) & cap_mask;
-    for (int probe = 0; probe < kMaxProbe;) {
+    uint64_t idx = probe_start<KW>(key, cap_mask);
+    int probe = 0;
+    // the prefetched slots: skip those holding other keys (key word 0 set
+    // and different), and start at the first empty or candidate one with
+    // its prefetched words (constant indices only: no register array is
+    // indexed at run time)
+    bool use_pre = false;
+    uint64_t pw[KW + 1];
+#pragma unroll
+    for (int w = 0; w <= KW; w++)
+        pw[w] = 0;
+    if (has_pre) {
+        int j0 = PFS;
+#pragma unroll
+        for (int t = 0; t < PFS; t++) {
+            const bool hit = j0 == PFS && (pre.w[t][0] == 0 || pre.w[t][0] == key[0]);
+            if (hit) {
+                j0 = t;
+#pragma unroll
+                for (int w = 0; w <= KW; w++)
+                    pw[w] = pre.w[t][w];
+            }
+        }
+        idx = (idx + j0) & cap_mask;
+        probe = j0;
+        use_pre = j0 < PFS;
+    }
+    for (; probe < kMaxProbe;) {
         uint64_t *s = table + idx * SW;
         // one plain (vector) read of the key words and best: it can only lag,
         // showing 0 for a key word being published or a larger best
         uint64_t wv[KW + 1];
-        if (KW <= 2 && has_pre) {
-            wv[0] = pre0;
-            wv[1] = pre1;
-            if constexpr (KW == 2)
-                wv[2] = pre2;
-            has_pre = false;
+        if (KW <= 2 && use_pre) {
+#pragma unroll
+            for (int w = 0; w <= KW; w++)
+                wv[w] = pw[w];
         } else {
             const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
             wv[0] = v0.x;
@@ -220,6 +270,7 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
                 }
             }
         }
+        use_pre = false;
         bool mine = false;
         if (wv[0] == 0) {
             const uint64_t prev = atomicCAS((unsigned long long *)s, 0ull, (unsigned long long)key[0]);
@@ -278,25 +329,27 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
     return -1;
 }
 
-// First-probe words of key's slot (key words + best, KW <= 2), for relax's
-// `pre`: issued before the parent's pair terms are staged, so the probe's
-// memory round trip overlaps the pair-table gathers.
-template <int KW>
-struct SlotWords {
-    uint64_t w0, w1, w2;
-};
-
-template <int KW>
-__device__ __forceinline__ SlotWords<KW> slot_prefetch(const uint64_t *__restrict__ table, uint64_t cap_mask,
-                                                       const uint64_t (&key)[KW])
+// Key words and best of the first PFS slots of key's probe sequence (one
+// cache line), for relax's `pre`: issued before the parent's pair terms are
+// staged, so the probe's memory round trip overlaps the pair-table gathers.
+template <int KW, int PFS>
+__device__ __forceinline__ SlotWords<KW, PFS> slot_prefetch(const uint64_t *__restrict__ table, uint64_t cap_mask,
+                                                            const uint64_t (&key)[KW])
 {
-    static_assert(KW <= 2, "prefetch covers 1- and 2-word keys");
+    static_assert(KW <= 2 && PFS <= line_slots<KW>() && (KW == 1 || PFS == 1),
+                  "prefetch: one line of 1-word keys, or one slot of a 2-word key");
     constexpr int SW = slot_words<KW>();
-    const uint64_t *s = table + (key_hash<KW>(key) & cap_mask) * SW;
-    const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
-    SlotWords<KW> o{v0.x, v0.y, 0};
-    if constexpr (KW == 2)
-        o.w2 = s[2];
+    const uint64_t *s0 = table + probe_start<KW>(key, cap_mask) * SW;
+    SlotWords<KW, PFS> o;
+#pragma unroll
+    for (int t = 0; t < PFS; t++) {
+        const uint64_t *s = s0 + t * SW;
+        const ulonglong2 v0 = *reinterpret_cast<const ulonglong2 *>(s);
+        o.w[t][0] = v0.x;
+        o.w[t][1] = v0.y;
+        if constexpr (KW == 2)
+            o.w[t][2] = s[2];
+    }
     return o;
 }
 
@@ -306,7 +359,7 @@ __device__ __forceinline__ int64_t lookup(const uint64_t *__restrict__ table, ui
                                           const uint64_t (&key)[KW])
 {
     constexpr int SW = slot_words<KW>();
-    uint64_t idx = key_hash<KW>(key) & cap_mask;
+    uint64_t idx = probe_start<KW>(key, cap_mask);
     for (int probe = 0; probe < kMaxProbe; probe++) {
         const uint64_t *s = table + idx * SW;
         if (s[0] == 0)

@@ -408,7 +408,7 @@ struct Ctl {
     alignas(128) unsigned long long k_start, k_end, expand_ticks, timed_launches;
     unsigned long long select_ticks, gap_ticks, prev_end;
     unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
-    unsigned long long body_ticks[8];   // profile: expand phases of block 0 (diagnostics)
+    unsigned long long body_ticks[12];  // profile: expand phases of block 0 (diagnostics)
     unsigned long long body_launches;
     int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step, pad1;
     unsigned long long dbg_w, dbg_r;
@@ -459,6 +459,10 @@ struct SearchArgs {
     int *goal_g;
     void *outbox;  // Remote<KW>[n_shards][outbox_cap]
     unsigned long long outbox_cap;
+    // the open-list capacities (= Ctl's), as kernel arguments: an append
+    // then computes its chunk-table address without a load of the control
+    // block ahead of the chunk-table read
+    unsigned long long maxch, pool_chunks;
 };
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
@@ -503,19 +507,19 @@ __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, 
 {
     const unsigned long long k = p >> kChunkLog2;
     const unsigned off = (unsigned)(p & (kChunk - 1));
-    const unsigned long long maxch = a.ctl->maxch;
+    const unsigned long long maxch = a.maxch;
     if (k >= maxch) {
         atomicAdd(&st->ovf_far, 1ull);
         return;
     }
     uint32_t *tp = a.chunk_tab + ((size_t)b * kSub + sq) * maxch + k;
-    if (off == 0) {
+    uint32_t c = 0;
+    if (off == 0) {  // the opener knows the id: no read-back
         const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
-        const uint32_t v = id < a.ctl->pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
-        __hip_atomic_store(tp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = id < a.pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
+        __hip_atomic_store(tp, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    uint32_t c;
-    while ((c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+    while (c == 0 && (c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
         __builtin_amdgcn_s_sleep(1);
     if (c == kNoChunk) {
         atomicAdd(&st->ovf_near, 1ull);
@@ -592,17 +596,17 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
 // All lanes of the wave must call it.
-template <int KW, typename PP>
+template <int KW, int PFS = 1, typename PP>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned long long &claimed, unsigned long long &ovf,
                                             const LocalPush<KW> &lp, bool remote_in = false, bool has_pre = false,
-                                            uint64_t pre0 = 0, uint64_t pre1 = 0, uint64_t pre2 = 0)
+                                            const SlotWords<KW, PFS> &pre = SlotWords<KW, PFS>{})
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
     if (valid && local) {
-        slot = relax<KW>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre0, pre1, pre2);
+        slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre);
         if (slot < 0) {
             ovf++;
             improved = false;
@@ -1005,6 +1009,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // child-slot prefetch: fixed N (the rounds of 64 children are static)
     // and 1- or 2-word keys
     constexpr bool kPf = N > 0 && KW <= 2;
+    // slots of the first probe line prefetched per child: the whole line
+    // for 1-word keys at N <= 5 (a collision then costs no round trip; a
+    // wave of 15-31 children almost always has one), one slot otherwise
+    // (register budget)
+    constexpr int kPfSlots = (KW == 1 && N > 0 && N <= 5) ? line_slots<KW>() : 1;
     Ctl *ctl = a.ctl;
     const DevProblem &Pg = *a.P;
     // the fields the level loop reads, in registers (KConst)
@@ -1115,7 +1124,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         BPHASE(1)
         // first-probe slot words of the first 64 children, read before the
         // pair terms are staged (one memory round trip less per level)
-        SlotWords<KW <= 2 ? KW : 1> pf{0, 0, 0};
+        SlotWords<KW, kPfSlots> pf{};
         bool has_pf = false;
         if (ok) {
             decode_key<N, KW>(P, n, par_.key, par_.pos);
@@ -1132,7 +1141,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                     const int m = glane;
                     uint64_t ck[KW];
                     child_key<N, KW>(P, n, par_.key, m, ck);
-                    pf = slot_prefetch<KW>(a.table, a.cap_mask, ck);
+                    pf = slot_prefetch<KW, kPfSlots>(a.table, a.cap_mask, ck);
                     has_pf = m >= 1 && m < masks && !(m & par_.blocked);
                 }
             };
@@ -1191,8 +1200,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                     owner = owner_dev<Parent<N, KW>::NMAX>(P, n, cp, P.n_shards);
                 }
             }
-            route_child<KW>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp, false,
-                            has_pf && r == 0, pf.w0, pf.w1, pf.w2);
+            BPHASE(8)
+            route_child<KW, kPfSlots>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp,
+                                      false, has_pf && r == 0, pf);
+            BPHASE(9)
         }
         BPHASE(7)
         lds_barrier();
@@ -1578,7 +1589,7 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
         }
         // lookup (backtrace.cpp:47-69 ClosedList find), slot words
         // [0, KW] = key + best in one read
-        uint64_t idx = key_hash<KW>(key) & cap_mask;
+        uint64_t idx = probe_start<KW>(key, cap_mask);
         int m = -1;
         for (int probe = 0; probe < kMaxProbe; probe++) {
             // the slot's key words and best in one round trip (plain loads

@@ -1004,6 +1004,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.goal_g = c->goal.p;
     a.outbox = c->outbox.p;
     a.outbox_cap = cfg.outbox_cap;
+    a.maxch = maxch_of(cfg);
+    a.pool_chunks = pool_chunks_of(cfg);
 
     const dim3 blk(kBlock);
     // about one resident wave of blocks: a block then walks several chunks
@@ -1279,7 +1281,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         for (int k = 0; k < 4; k++)
             std::fprintf(stderr, " %.2f", (double)h.phase_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.timed_launches));
         std::fprintf(stderr, "\n[pastar] expand phases of block 0 (us/launch):");
-        for (int k = 0; k < 8; k++)
+        for (int k = 0; k < 10; k++)
             std::fprintf(stderr, " %.2f", (double)h.body_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.body_launches));
         std::fprintf(stderr, "\n");
     }
