@@ -1070,3 +1070,247 @@ int64_t orc_alignment_cost(const orc_problem *p, const char *aln, int stride, in
             return -1;
     return g;
 }
+
+/* ------------------------------------------------------------------ */
+/* Multithreaded PAStar (the reference's -t T, one rank)               */
+/* ------------------------------------------------------------------ */
+
+/* PAStar<N>::worker_inner (PAStar.cpp:320-401) over T threads: thread t owns
+ * the coordinates with get_id(c, T) == t (FZORDER, shift 12, Node.cpp:244);
+ * each holds its own open and closed lists (an astate, as in orc_astar) and
+ * an inbox that the other threads append to (the reference's per-thread
+ * queue_mutex-protected vectors, PAStar.cpp:366-396).  Used as the timed
+ * multicore CPU baseline (-t $(nproc)); expansions and
+ * order are non-deterministic, the score is exact.
+ *
+ * Goal and stop (PAStar.cpp:410-547, restated): the goal's owner records
+ * g(goal) in `best` when it pops it (h(goal) = 0); a node with f >= best is
+ * never expanded.  A thread is idle when its open list has nothing below
+ * best and its inbox and outgoing buffers are empty.  Termination is the
+ * counting test: read the received count, then every idle flag, then the
+ * sent count; stop iff all idle and received == sent.  Senders count a
+ * message before it becomes visible, and a receiver clears its idle flag
+ * before it counts a receipt, which makes the test sound. */
+
+#include <pthread.h>
+#include <sched.h>
+#include <stdatomic.h>
+
+typedef struct mt_inbox {
+    pthread_mutex_t mu;
+    orc_node *v;
+    size_t n, cap;
+    atomic_llong avail; /* n, readable without the lock (a hint) */
+} mt_inbox;
+
+typedef struct mt_shared {
+    const orc_problem *p;
+    int T;
+    mt_inbox *inbox;
+    atomic_int *idle;
+    atomic_llong sent, received, best, expansions, reopen;
+    atomic_int stop;
+} mt_shared;
+
+typedef struct mt_arg {
+    mt_shared *sh;
+    int t;
+} mt_arg;
+
+static void vec_push(orc_node **v, size_t *n, size_t *cap, const orc_node *x)
+{
+    if (*n == *cap) {
+        *cap = *cap ? *cap * 2 : 256;
+        *v = (orc_node *)realloc(*v, sizeof(orc_node) * *cap);
+    }
+    (*v)[(*n)++] = *x;
+}
+
+static void mt_flush(mt_shared *sh, orc_node **out, size_t *out_n, size_t *out_cap)
+{
+    for (int d = 0; d < sh->T; d++) {
+        if (!out_n[d])
+            continue;
+        atomic_fetch_add(&sh->sent, (long long)out_n[d]); /* counted before visible */
+        mt_inbox *ib = &sh->inbox[d];
+        pthread_mutex_lock(&ib->mu);
+        for (size_t k = 0; k < out_n[d]; k++)
+            vec_push(&ib->v, &ib->n, &ib->cap, &out[d][k]);
+        atomic_store(&ib->avail, (long long)ib->n);
+        pthread_mutex_unlock(&ib->mu);
+        out_n[d] = 0;
+    }
+    (void)out_cap;
+}
+
+static void *mt_worker(void *argp)
+{
+    mt_arg *arg = (mt_arg *)argp;
+    mt_shared *sh = arg->sh;
+    const orc_problem *p = sh->p;
+    const int t = arg->t, T = sh->T, n = p->n;
+    astate s;
+    memset(&s, 0, sizeof(s));
+    s.n = n;
+    s.caprec = 1 << 14;
+    s.recs = (rec *)malloc(sizeof(rec) * s.caprec);
+    s.tcap = 1 << 15;
+    s.tab = (uint32_t *)calloc(s.tcap, sizeof(uint32_t));
+    s.capheap = 1 << 14;
+    s.heap = (hent *)malloc(sizeof(hent) * s.capheap);
+    orc_node **out = (orc_node **)calloc((size_t)T, sizeof(orc_node *));
+    size_t *out_n = (size_t *)calloc((size_t)T, sizeof(size_t));
+    size_t *out_cap = (size_t *)calloc((size_t)T, sizeof(size_t));
+    orc_node *drain = NULL;
+    size_t drain_cap = 0;
+    orc_node *neigh = (orc_node *)malloc(sizeof(orc_node) * ((size_t)1 << n));
+    int *owner = (int *)malloc(sizeof(int) * ((size_t)1 << n));
+    uint16_t goal[ORC_MAX_SEQ] = {0};
+    for (int i = 0; i < n; i++)
+        goal[i] = (uint16_t)p->len[i];
+    int64_t expansions = 0, reopen = 0;
+    int since_flush = 0;
+    while (!atomic_load(&sh->stop)) {
+        /* consume the inbox (PAStar::enqueue of received nodes) */
+        mt_inbox *ib = &sh->inbox[t];
+        size_t got = 0;
+        if (atomic_load(&ib->avail)) {
+            pthread_mutex_lock(&ib->mu);
+            got = ib->n;
+            if (got) {
+                orc_node *tmp = ib->v;
+                size_t tcap = ib->cap;
+                ib->v = drain;
+                ib->cap = drain_cap;
+                ib->n = 0;
+                drain = tmp;
+                drain_cap = tcap;
+            }
+            atomic_store(&ib->avail, 0);
+            pthread_mutex_unlock(&ib->mu);
+        }
+        if (got) {
+            atomic_store(&sh->idle[t], 0); /* before the receipt is counted */
+            atomic_fetch_add(&sh->received, (long long)got);
+            long long best = atomic_load(&sh->best);
+            for (size_t k = 0; k < got; k++)
+                if (drain[k].f < best)
+                    enqueue_node(&s, &drain[k], &reopen);
+        }
+        long long best = atomic_load(&sh->best);
+        if (open_min_f(&s) < best) {
+            atomic_store(&sh->idle[t], 0);
+            int64_t ci = open_dequeue(&s);
+            expansions++;
+            rec *cur = &s.recs[ci];
+            cur->state = 2;
+            if (!memcmp(cur->pos, goal, sizeof(uint16_t) * (size_t)n)) {
+                long long g = cur->g, old = atomic_load(&sh->best);
+                while (g < old && !atomic_compare_exchange_weak(&sh->best, &old, g))
+                    ;
+                continue;
+            }
+            orc_node node;
+            memcpy(node.pos, cur->pos, sizeof(node.pos));
+            node.g = cur->g;
+            node.f = cur->f;
+            node.parenti = cur->parenti;
+            int cnt = orc_get_neigh(p, &node, T, ORC_HASH_FZORDER, 12, neigh, owner);
+            for (int k = 0; k < cnt; k++) {
+                if (neigh[k].f >= best)
+                    continue;
+                if (owner[k] == t)
+                    enqueue_node(&s, &neigh[k], &reopen);
+                else
+                    vec_push(&out[owner[k]], &out_n[owner[k]], &out_cap[owner[k]], &neigh[k]);
+            }
+            if (++since_flush >= 8) {
+                mt_flush(sh, out, out_n, out_cap);
+                since_flush = 0;
+            }
+            continue;
+        }
+        /* nothing below best here: hand over what is buffered, go idle */
+        mt_flush(sh, out, out_n, out_cap);
+        since_flush = 0;
+        pthread_mutex_lock(&ib->mu);
+        int empty = ib->n == 0;
+        if (empty)
+            atomic_store(&sh->idle[t], 1);
+        pthread_mutex_unlock(&ib->mu);
+        if (!empty)
+            continue;
+        /* counting termination test */
+        long long r = atomic_load(&sh->received);
+        int all = 1;
+        for (int d = 0; d < T && all; d++)
+            all = atomic_load(&sh->idle[d]);
+        long long sn = atomic_load(&sh->sent);
+        if (all && r == sn) {
+            atomic_store(&sh->stop, 1);
+            break;
+        }
+        sched_yield();
+    }
+    atomic_fetch_add(&sh->expansions, expansions);
+    atomic_fetch_add(&sh->reopen, reopen);
+    for (int d = 0; d < T; d++)
+        free(out[d]);
+    free(out);
+    free(out_n);
+    free(out_cap);
+    free(drain);
+    free(neigh);
+    free(owner);
+    free(s.recs);
+    free(s.tab);
+    free(s.heap);
+    return NULL;
+}
+
+int orc_pastar_mt(const orc_problem *p, int threads, orc_result *res)
+{
+    memset(res, 0, sizeof(*res));
+    if (threads < 1 || threads > 1024)
+        return -1;
+    mt_shared sh;
+    memset(&sh, 0, sizeof(sh));
+    sh.p = p;
+    sh.T = threads;
+    sh.inbox = (mt_inbox *)calloc((size_t)threads, sizeof(mt_inbox));
+    sh.idle = (atomic_int *)calloc((size_t)threads, sizeof(atomic_int));
+    for (int t = 0; t < threads; t++)
+        pthread_mutex_init(&sh.inbox[t].mu, NULL);
+    atomic_store(&sh.best, INT64_MAX);
+    /* the origin on its owner (PAStar.cpp:153) */
+    orc_node zero;
+    orc_initial_node(p, &zero);
+    int own0 = orc_get_id(p->n, zero.pos, threads, ORC_HASH_FZORDER, 12);
+    atomic_fetch_add(&sh.sent, 1);
+    vec_push(&sh.inbox[own0].v, &sh.inbox[own0].n, &sh.inbox[own0].cap, &zero);
+    atomic_store(&sh.inbox[own0].avail, 1);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    mt_arg *args = (mt_arg *)malloc(sizeof(mt_arg) * (size_t)threads);
+    double t0 = now_s();
+    for (int t = 0; t < threads; t++) {
+        args[t].sh = &sh;
+        args[t].t = t;
+        pthread_create(&th[t], NULL, mt_worker, &args[t]);
+    }
+    for (int t = 0; t < threads; t++)
+        pthread_join(th[t], NULL);
+    res->seconds = now_s() - t0;
+    res->expansions = atomic_load(&sh.expansions);
+    res->reopen = atomic_load(&sh.reopen);
+    long long best = atomic_load(&sh.best);
+    res->score = best;
+    for (int t = 0; t < threads; t++) {
+        free(sh.inbox[t].v);
+        pthread_mutex_destroy(&sh.inbox[t].mu);
+    }
+    free(sh.inbox);
+    free((void *)sh.idle);
+    free(th);
+    free(args);
+    return best == INT64_MAX ? -1 : 0;
+}

@@ -89,6 +89,12 @@ void orc_initial_node(const orc_problem *p, orc_node *out);
  * Returns 0 on success. */
 int orc_astar(const orc_problem *p, orc_result *res, char *aln, int aln_cap);
 
+/* Multithreaded PAStar (-t threads, one rank; PAStar.cpp:320-547): z-order
+ * owned open/closed lists per thread, inbox exchange, counting termination.
+ * The timed multicore CPU baseline; score exact, expansions vary run to run.
+ * Returns 0 on success. */
+int orc_pastar_mt(const orc_problem *p, int threads, orc_result *res);
+
 /* SP cost of a given alignment (rows of equal length) under the same
  * weighted edge costs (Node.cpp:130-152 summed along the path). */
 int64_t orc_alignment_cost(const orc_problem *p, const char *aln, int aln_stride, int cols);

@@ -62,6 +62,7 @@ def lib():
                                     ctypes.POINTER(orc_node), ctypes.POINTER(ctypes.c_int)]
         L.orc_initial_node.argtypes = [P, ctypes.POINTER(orc_node)]
         L.orc_astar.argtypes = [P, ctypes.POINTER(orc_result), ctypes.c_char_p, ctypes.c_int]
+        L.orc_pastar_mt.argtypes = [P, ctypes.c_int, ctypes.POINTER(orc_result)]
         L.orc_alignment_cost.restype = ctypes.c_int64
         L.orc_alignment_cost.argtypes = [P, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.orc_cost.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -143,6 +144,14 @@ class Oracle:
         rows = [buf.raw[i * cap:i * cap + r.aln_len].decode("latin-1") for i in range(self.n)]
         return {"score": r.score, "expansions": r.expansions, "reopen": r.reopen, "open_size": r.open_size,
                 "closed_size": r.closed_size, "similarity": r.similarity, "seconds": r.seconds, "rows": rows}
+
+    def pastar_mt(self, threads):
+        """Multithreaded PAStar -t threads (score exact, expansions vary)."""
+        r = orc_result()
+        rc = lib().orc_pastar_mt(self.p, int(threads), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError("oracle parallel search failed (%d)" % rc)
+        return {"score": r.score, "expansions": r.expansions, "reopen": r.reopen, "seconds": r.seconds}
 
     def alignment_cost(self, rows):
         cols = len(rows[0])

@@ -112,6 +112,21 @@ def test_serial_search_matches_reference(name, kat):
     assert [row.replace("-", "") for row in r["rows"]] == o.seqs
 
 
+@pytest.mark.parametrize("threads", [1, 2, 4])
+@pytest.mark.parametrize("name", SMALL)
+def test_multithreaded_search_score(name, threads, kat):
+    """The multithreaded restatement (the -t T CPU baseline): exact score at
+    any thread count; at one thread it expands exactly the serial count."""
+    ref = kat["inputs"][name]
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    r = o.pastar_mt(threads)
+    assert r["score"] == ref["score"]
+    if threads == 1:
+        assert r["expansions"] == ref["expansions_t1"]
+    else:
+        assert r["expansions"] >= ref["expansions_t1"] // 2
+
+
 @pytest.mark.slow
 def test_serial_search_kinase(kat):
     """kinase at -t 1: 4 497 279 expansions, score 421546 (about 40 s)."""
