@@ -1172,7 +1172,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             }
             ok = verdict != 0;
         }
-        lds_barrier();
+        // a wave reads only the terms it staged itself (terms_all[wave]):
+        // its own LDS writes landing is enough, no block barrier
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         BPHASE(2)
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
@@ -1206,8 +1208,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             BPHASE(9)
         }
         BPHASE(7)
-        lds_barrier();
-        BPHASE(3)
     };
 
     // level 0: this block's share of the batch; levels 1..depth-1: the
@@ -1259,9 +1259,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             e_nx = batch_entry(a, view, prefix, bstart, nn);
         process(ok, e, ps, no_le, false, lp);
     }
+    // the continuation queue and the deferred entries are block-wide: one
+    // barrier per level, after all of its chunks
+    lds_barrier();
+    BPHASE(3)
     int cur = 0;
     for (int lvl = 1; lvl < depth; lvl++) {
-        const int cnt = lq_count[cur] < lq_cap ? lq_count[cur] : lq_cap;  // read after process's barrier
+        const int cnt = lq_count[cur] < lq_cap ? lq_count[cur] : lq_cap;  // read after the level's barrier
         if (cnt == 0)
             break;
         const int nxt = cur ^ 1;
@@ -1275,6 +1279,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             const bool ok = idx < cnt;
             process(ok, Entry{0, 0}, no_ps, ok ? lq[cur][idx] : no_le, true, lq_next);
         }
+        lds_barrier();
+        BPHASE(3)
         cur = nxt;
     }
     // the deferred open-list entries: ranked per bucket in LDS, then one
