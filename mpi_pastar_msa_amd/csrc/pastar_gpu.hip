@@ -1334,7 +1334,10 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.eager = o.eager;
     if (o.depth < 0 || o.depth > 64)
         return fail(PASTAR_EINVAL, "depth %d outside [0, 64]", o.depth);
-    cfg.depth = o.depth > 0 ? o.depth : 8;
+    // levels per launch: 8, and 24 for N = 3, whose expansions are cheapest
+    // (7 children; PF08184 0.40 -> 0.28 ms; N = 4 is best at 8: syn4x200
+    // 2.0 ms at 8, 2.2-2.5 ms at 12-24)
+    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 24 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     int rc = PASTAR_OK, retries = 0;
