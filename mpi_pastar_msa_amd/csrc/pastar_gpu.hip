@@ -904,7 +904,11 @@ int estimate_band_log2(pastar_ctx *c, int h0, int64_t band_opt, int *w_out)
         int64_t sum = 0;
         for (int64_t k = 0; k < cnt; k++)
             sum += (int64_t)kids[(size_t)k].f - h0;
-        band = cnt ? std::max<int64_t>(1, sum / cnt / 3) : 1;
+        // an eighth of the mean f increase of the origin's children: the
+        // best or tied-best width on every workload (profiles/r1_tune_*.txt:
+        // kinase 30 -> 21 ms, syn4x200 1.9 -> 1.5 ms with fewer expansions,
+        // PF08184 61 expansions for 60 serial, syn8x400 equal)
+        band = cnt ? std::max<int64_t>(1, sum / cnt / 8) : 1;
     }
     int w = 0;
     while ((2ll << w) <= band * 4 / 3 && w < 24)  // nearest power of two
@@ -1314,7 +1318,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         o = *opts;
     SearchCfg cfg;
     const unsigned long long masks = (1ull << c->n) - 1;
-    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 32768ull;
+    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : 65536ull;
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     // default node-table size: learned from the last search on this context
     // (a repeated search of the same problem initialises only what it

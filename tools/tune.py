@@ -17,7 +17,7 @@ from mpi_pastar_msa_amd import Engine, PAStarOpt, Sequences  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("workload")
 ap.add_argument("--mult", default="0.125,0.25,0.5,1,2")
-ap.add_argument("--batch", default="32768")
+ap.add_argument("--batch", default="65536")
 ap.add_argument("--kmin", type=int, default=0)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--table-log2", type=int, default=0)
