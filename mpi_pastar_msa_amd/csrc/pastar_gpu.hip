@@ -972,12 +972,13 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     {
         // block-local continuation pays where an expansion is cheap (few
-        // children, a narrow frontier: PF08184 2x, syn4x200 1.4x) and costs
-        // where the fan-out is wide (kinase neutral at 16 rounds, syn8x400
-        // 1.7x slower at 2): the minimum rounds a level must be allowed
-        // before a launch continues, by N (profiles/r1_depth_sweep.txt)
+        // children, a narrow frontier: PF08184 2x, syn4x200 1.4x; kinase 8%
+        // at 1 round with the 1/8 band) and costs where the fan-out is wide
+        // (syn8x400 1.25x slower at any setting): the minimum rounds a level
+        // must be allowed before a launch continues, by N
+        // (profiles/r1_depth_sweep.txt, profiles/r1_rounds_sweep.txt)
         const char *e = std::getenv("PASTAR_DEEP_ROUNDS");  // tuning override
-        hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 4 ? 2 : c->n <= 6 ? 16 : (1 << 30));
+        hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 4 ? 2 : c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
     // uploads from pinned staging, stream-ordered (no host round trip
