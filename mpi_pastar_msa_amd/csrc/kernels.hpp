@@ -61,6 +61,9 @@ __host__ __device__ constexpr size_t pairalign_lds_bytes(int maxl2, int alpha, b
 // then an LDS read, and the per-step waits never include the stores).
 // WRITE_H: also store the plain table H (only pastar_gpu_pair_table reads it;
 // the search and h read HC).
+// EQ_GAPS: gap open == gap extension (the reference's constants, Cost.h:13):
+// the gap direction cannot change a value, so it is not tracked (a third
+// fewer instructions per cell on the dependent chain).
 //
 // Stores: a lane owns one row, so a per-step store touches 64 rows (64 cache
 // lines) for 4-8 B each and the CU's address path, not HBM, bounds the sweep.
@@ -69,7 +72,7 @@ __host__ __device__ constexpr size_t pairalign_lds_bytes(int maxl2, int alpha, b
 constexpr int kPaChunk = 8;
 typedef int pa_v4i __attribute__((ext_vector_type(4), aligned(8)));
 
-template <bool SUB_LDS, bool WRITE_H>
+template <bool SUB_LDS, bool WRITE_H, bool EQ_GAPS>
 __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const DevProblem *__restrict__ Pp,
                                                                        int32_t *__restrict__ H,
                                                                        int2 *__restrict__ HC)
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 const int jc = jj < 0 ? 0 : (jj > L2 ? L2 : jj);
                 const int jn = jj - 1 < 0 ? 0 : (jj - 1 > L2 ? L2 : jj - 1);
                 lb[u] = below[jc];
-                lbd[u] = belowd[jc];
+                lbd[u] = EQ_GAPS ? 0 : belowd[jc];
                 nc[u] = s2[jn];
             }
 #pragma unroll
@@ -166,15 +169,15 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 // only cells inside the table are kept.  Steps past the sweep
                 // (t >= nsteps) have j < 0 on every lane and change nothing.
                 const bool in = row_ok && j >= 0 && j <= L2;
-                const int m_up = from_lane_above(m), a_up = from_lane_above(a);
+                const int m_up = from_lane_above(m), a_up = EQ_GAPS ? 0 : from_lane_above(a);
                 diag = down;
                 down = use_lds_below ? lb[u] : m_up;
-                adown = use_lds_below ? lbd[u] : a_up;
+                adown = EQ_GAPS ? 0 : (use_lds_below ? lbd[u] : a_up);
                 const int cost_here = cost;
                 cost = nc[u];
                 const int right = m, aright = a;
-                const int c0 = down + (adown == kGapX ? GE : GO);
-                const int c1 = right + (aright == kGapY ? GE : GO);
+                const int c0 = down + (EQ_GAPS ? GO : (adown == kGapX ? GE : GO));
+                const int c1 = right + (EQ_GAPS ? GO : (aright == kGapY ? GE : GO));
                 int mm = c0 < c1 ? c0 : c1;
                 int aa = c0 < c1 ? kGapX : kGapY;
                 const int c2 = diag + cost_here;
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
                 cb[u] = make_int2(mm * wgt, cost_here * wgt);
                 m = in ? mm : m;
-                a = in ? aa : a;
+                a = EQ_GAPS ? 0 : (in ? aa : a);
                 tb[u] = m;
                 tbd[u] = a;
                 if constexpr (WRITE_H)
@@ -203,7 +206,8 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                     const int jj = j0 - u;
                     if (row_ok && jj >= 0 && jj <= L2) {
                         top[jj] = tb[u];
-                        topd[jj] = (uint8_t)tbd[u];
+                        if constexpr (!EQ_GAPS)
+                            topd[jj] = (uint8_t)tbd[u];
                     }
                 }
                 *my_progress = (band << 16) | (t0 + kPaChunk < nsteps ? t0 + kPaChunk : nsteps);

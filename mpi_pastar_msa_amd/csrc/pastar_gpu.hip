@@ -680,10 +680,18 @@ static int launch_pairalign(pastar_ctx *c, bool write_h)
     const size_t lds = pairalign_lds_bytes(maxl2, c->hp.alpha, sub_lds);
     if (lds > 160 * 1024)
         return fail(PASTAR_EINVAL, "sequence too long for the LDS wavefront (%d)", maxl2);
-    const void *fn = sub_lds ? (write_h ? (const void *)pairalign_wave_kernel<true, true>
-                                        : (const void *)pairalign_wave_kernel<true, false>)
-                             : (write_h ? (const void *)pairalign_wave_kernel<false, true>
-                                        : (const void *)pairalign_wave_kernel<false, false>);
+    // the reference's gap constants are equal (Cost.h:13); the general form
+    // stays for patched constants
+    const bool eq = c->hp.gap_open == c->hp.gap_ext;
+    const void *fn =
+        sub_lds ? (write_h ? (eq ? (const void *)pairalign_wave_kernel<true, true, true>
+                                 : (const void *)pairalign_wave_kernel<true, true, false>)
+                           : (eq ? (const void *)pairalign_wave_kernel<true, false, true>
+                                 : (const void *)pairalign_wave_kernel<true, false, false>))
+                : (write_h ? (eq ? (const void *)pairalign_wave_kernel<false, true, true>
+                                 : (const void *)pairalign_wave_kernel<false, true, false>)
+                           : (eq ? (const void *)pairalign_wave_kernel<false, false, true>
+                                 : (const void *)pairalign_wave_kernel<false, false, false>));
     if (lds > 64 * 1024)
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p};

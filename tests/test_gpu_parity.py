@@ -36,6 +36,19 @@ def test_pairalign_tables_bit_exact(name, kat, oracles):
             np.testing.assert_array_equal(e.pair_table(k), o.pair_table(k))
 
 
+@pytest.mark.parametrize("gaps", [(35, 25), (20, 40), (30, 30)])
+@pytest.mark.parametrize("name", ["PF08184", "syn4x200_s1"])
+def test_pairalign_patched_gap_constants(name, gaps, kat, oracles):
+    """PairAlign with gap open != gap extension (the general affine form the
+    reference keeps patchable, PairAlign.cpp:96-101) against the oracle."""
+    o = oracles[name]
+    go, ge = gaps
+    with _engine(name, kat, gap_open=go, gap_ext=ge) as e:
+        for k in range(e.npairs):
+            x, y = o.pairs[k]
+            np.testing.assert_array_equal(e.pair_table(k), orc.pairalign(o.seqs[x], o.seqs[y], go, ge))
+
+
 @pytest.mark.parametrize("name", SMALL + ["kinase"])
 def test_h_origin_and_first_expansion(name, kat, oracles):
     ref = kat["inputs"][name]
