@@ -156,6 +156,31 @@ def test_random_small_problems_match_oracle():
             assert o.alignment_cost(rows) == ref["score"]
 
 
+def test_random_edge_problems_match_oracle():
+    """Edge shapes: 7 and 8 sequences (the multi-round child loop with 1-word
+    keys), ragged lengths (1 residue beside 40), and residues the reference
+    costs 0 (B J O U X Z and lower case, Cost.cpp:10-262)."""
+    rng = random.Random(11)
+    odd = "ACDEFGHIKLMNPQRSTVWY" + "BJOUXZ" + "acdwxy"
+    cases = []
+    for n in (7, 8):
+        cases.append(["".join(rng.choice(odd) for _ in range(rng.randint(1, 7))) for _ in range(n)])
+    for n in (3, 4, 5):
+        lens = [1] + [rng.randint(20, 40) for _ in range(n - 1)]
+        rng.shuffle(lens)
+        cases.append(["".join(rng.choice(odd) for _ in range(L)) for L in lens])
+    for seqs in cases:
+        o = orc.Oracle(seqs=seqs)
+        ref = o.astar()
+        with Engine(seqs).init() as e:
+            assert e.weight_matrix == o.weights
+            r = e.pa_star(PAStarOpt())
+            assert r.score == ref["score"], (seqs, r, ref)
+            rows = e.alignment()
+            assert o.alignment_cost(rows) == ref["score"]
+            assert [row.replace("-", "") for row in rows] == seqs
+
+
 def test_capacity_autogrow(kat):
     """Starting from tiny capacities the engine grows the exhausted buffer and
     restarts; the result is unchanged."""
