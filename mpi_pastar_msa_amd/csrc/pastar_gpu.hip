@@ -986,7 +986,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // must be allowed before a launch continues, by N
         // (profiles/r1_depth_sweep.txt, profiles/r1_rounds_sweep.txt)
         const char *e = std::getenv("PASTAR_DEEP_ROUNDS");  // tuning override
-        hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 4 ? 2 : c->n <= 6 ? 1 : (1 << 30));
+        hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
     // uploads from pinned staging, stream-ordered (no host round trip
@@ -1123,8 +1123,12 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         long long steps_before = 0;
         int rc = PASTAR_OK;
         for (;;) {
-            // long runs until the predicted end is near, then short ones
-            const bool near_end = c->last_steps > 0 && steps_before + kLong > c->last_steps + kShort;
+            // long runs until the predicted end is near, then short ones: a
+            // launch past the end exits at once (a few us), a replay costs a
+            // host round trip (~20 us), so a long run may overshoot the
+            // predicted end by up to 16 launches
+            constexpr int kOvershoot = 16;
+            const bool near_end = c->last_steps > 0 && steps_before + kLong > c->last_steps + kOvershoot;
             const int S = near_end ? kShort : kLong;
             hipError_t e = use_graph ? hipGraphLaunch(c->step_exec[near_end ? 1 : 0], c->stream) : enqueue_steps(S);
             if (e == hipSuccess)
@@ -1349,10 +1353,10 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.eager = o.eager;
     if (o.depth < 0 || o.depth > 64)
         return fail(PASTAR_EINVAL, "depth %d outside [0, 64]", o.depth);
-    // levels per launch: 8, and 24 for N = 3, whose expansions are cheapest
-    // (7 children; PF08184 0.40 -> 0.28 ms; N = 4 is best at 8: syn4x200
-    // 2.0 ms at 8, 2.2-2.5 ms at 12-24)
-    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 24 : 8);
+    // levels per launch: the cheaper an expansion, the deeper (PF08184 0.40
+    // -> 0.25 ms at 24; syn4x200 1.52 -> 1.44 ms at 12 with one round;
+    // profiles/r1_depth_sweep.txt)
+    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 24 : c->n == 4 ? 12 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     int rc = PASTAR_OK, retries = 0;
