@@ -697,7 +697,11 @@ static int launch_pairalign(pastar_ctx *c, bool write_h)
     void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p};
     HIP_TRY(hipLaunchKernel(fn, dim3(c->npairs), dim3(64 * kPaWaves), args, lds, c->stream));
     PA_TRY(check_launch());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the search and h run on the same stream, so the search-form tables
+    // need no host wait (the first search step overlaps this launch's tail);
+    // the plain tables are read back by the caller
+    if (write_h)
+        HIP_TRY(hipStreamSynchronize(c->stream));
     return PASTAR_OK;
 }
 
