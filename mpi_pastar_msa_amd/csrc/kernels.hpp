@@ -985,23 +985,35 @@ __device__ __forceinline__ PSlot<KW> load_pslot(const uint64_t *__restrict__ tab
     return o;
 }
 
-// Entry i of the current batch (binary search over the range prefix in LDS).
-__device__ __forceinline__ Entry batch_entry(const SearchArgs &a, const SelView &v, const unsigned long long *prefix,
-                                             const unsigned long long *bstart, unsigned long long i)
+// Range of batch entry i (wave-uniform call): the batch's range prefix is
+// held two entries per lane (pf_lo = prefix[2 lane], pf_hi = prefix[2 lane +
+// 1], constant for the launch), so "the last range r with prefix[r] <= i" is
+// a count of set ballot bits, for each of the wave's npw entries in turn --
+// no chain of dependent LDS reads.  Empty ranges repeat a prefix value and
+// are skipped the same way the binary search skips them.
+__device__ __forceinline__ int batch_range(uint32_t pf_lo, uint32_t pf_hi, unsigned long long i, int npw, int lpn)
 {
-    int lo = 0, hi = kRanges - 1;  // last range with prefix[r] <= i
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (prefix[mid] <= i)
-            lo = mid;
-        else
-            hi = mid - 1;
+    const int lane = lane_id();
+    int r = 0;
+    for (int g = 0; g < npw; g++) {
+        const unsigned long long ig = __shfl(i, g * lpn);
+        const int cnt = __popcll(__ballot(pf_lo <= ig)) + __popcll(__ballot(pf_hi <= ig));
+        if (lane / lpn == g)
+            r = cnt - 1;
     }
-    const int r = lo, bb = v.batch_b + r / kSub, sq = r % kSub;
+    return r;
+}
+
+// Entry i of the current batch, in range r.
+__device__ __forceinline__ Entry batch_entry_at(const SearchArgs &a, const SelView &v, const uint32_t *prefix,
+                                                const unsigned long long *bstart, unsigned long long i, int r)
+{
+    const int bb = v.batch_b + r / kSub, sq = r % kSub;
     const unsigned long long p = bstart[r] + (i - prefix[r]);
     const uint32_t c = a.chunk_tab[((size_t)bb * kSub + sq) * v.maxch + (p >> kChunkLog2)];
     return a.pool[(size_t)(c - 1) * kChunk + (p & (kChunk - 1))];
 }
+
 
 // expand every entry of the batch (worker_inner's dequeue, closed check and
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
@@ -1045,12 +1057,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
     __shared__ int2 terms_all[kWaves][terms_per_wave(N)];
-    __shared__ unsigned long long prefix[kRanges + 1], bstart[kRanges];
+    // batch offsets fit 32 bits (batch_nodes <= 2^30, checked on the host)
+    __shared__ uint32_t prefix[kRanges + 1];
+    __shared__ unsigned long long bstart[kRanges];
     __shared__ PairConst pc[kMaxPairs];
     int2 *terms = &terms_all[wave][group * 4 * npairs];
     // one round trip: the batch's ranges and the pair constants
     for (int r = threadIdx.x; r <= kRanges; r += blockDim.x) {
-        prefix[r] = ctl->b_prefix[r];
+        prefix[r] = (uint32_t)ctl->b_prefix[r];
         if (r < kRanges)
             bstart[r] = ctl->b_start[r];
     }
@@ -1245,11 +1259,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // chunk waits for one memory round trip before staging, not three
     // (entry: chunk table + pool, then the slot)
     const PSlot<KW> no_ps{};
+    const uint32_t pf_lo = prefix[2 * lane], pf_hi = prefix[2 * lane + 1];
     Entry e_nx{0, 0};
     {
         const unsigned long long node = (unsigned long long)blockIdx.x * per_block + wave * npw + group;
+        const int r = batch_range(pf_lo, pf_hi, node, npw, lpn);
         if (node < nb)
-            e_nx = batch_entry(a, view, prefix, bstart, node);
+            e_nx = batch_entry_at(a, view, prefix, bstart, node, r);
     }
     for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
         const unsigned long long node = chunk * per_block + wave * npw + group;
@@ -1259,8 +1275,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if (ok)
             ps = load_pslot<KW>(a.table, e.slot);
         const unsigned long long nn = node + (unsigned long long)gridDim.x * per_block;
+        const int r = batch_range(pf_lo, pf_hi, nn, npw, lpn);
         if (nn < nb)
-            e_nx = batch_entry(a, view, prefix, bstart, nn);
+            e_nx = batch_entry_at(a, view, prefix, bstart, nn, r);
         process(ok, e, ps, no_le, false, lp);
     }
     // the continuation queue and the deferred entries are block-wide: one

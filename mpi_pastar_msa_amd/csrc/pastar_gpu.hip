@@ -1337,6 +1337,8 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     const unsigned long long masks = (1ull << c->n) - 1;
     // most parents per step: 131072 up to N = 6 (kinase 20.2 -> 18.4 ms),
     // 65536 beyond (syn8x400 72 ms at 65536, 73.5 at 131072)
+    if (o.batch_nodes > (1ll << 30))  // batch offsets are 32-bit on the device
+        return fail(PASTAR_EINVAL, "batch_nodes %lld above 2^30", (long long)o.batch_nodes);
     cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : (c->n <= 6 ? 131072ull : 65536ull);
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     // default node-table size: learned from the last search on this context
