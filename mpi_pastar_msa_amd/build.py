@@ -21,6 +21,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # arithmetic (no FMA contraction), as the reference's g++ build computes it.
 COMMON = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+# diagnostics builds, e.g. PASTAR_HIPCC_FLAGS=-DPASTAR_PHASE_TIMERS (block-0
+# phase timers of the expand kernel, read with PASTAR_TIMING_MASK=5)
+COMMON += os.environ.get("PASTAR_HIPCC_FLAGS", "").split()
 
 LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp"]
 LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp"]

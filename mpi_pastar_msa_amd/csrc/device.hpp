@@ -399,7 +399,7 @@ __device__ __forceinline__ KConst<N, KW> load_kconst(const DevProblem &P)
 #pragma unroll
     for (int i = 0; i < KConst<N, KW>::NMAX; i++) {
         k.len[i] = P.len[i];
-        k.kword[i] = P.kword[i];
+        k.kword[i] = KW == 1 ? 0 : P.kword[i];
         k.kshift[i] = P.kshift[i];
         k.kbits[i] = P.kbits[i];
     }
@@ -487,7 +487,7 @@ __device__ __forceinline__ void decode_key(const PP &P, int n, const uint64_t (&
             pos[i] = 0;
             continue;
         }
-        const int w = P.kword[i];
+        const int w = KW == 1 ? 0 : P.kword[i];  // one word: no table read
         uint64_t word = key[0];
 #pragma unroll
         for (int k = 1; k < KW; k++)
@@ -633,7 +633,7 @@ __device__ __forceinline__ void child_key(const PP &P, int n, const uint64_t (&k
         if ((N == 0 && i >= n) || !((m >> i) & 1))
             continue;
         const uint64_t inc = 1ull << P.kshift[i];
-        const int w = P.kword[i];
+        const int w = KW == 1 ? 0 : P.kword[i];  // one word: no table read
 #pragma unroll
         for (int k = 0; k < KW; k++)
             if (w == k)

@@ -1069,6 +1069,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             bstart[r] = ctl->b_start[r];
     }
     stage_pairs(Pg, pc);
+    // block 0's phase timers (diagnostics, PASTAR_TIMING_MASK bit 2): built
+    // only with -DPASTAR_PHASE_TIMERS, since their 64-bit clocks are held in
+    // scalar registers through the whole level loop
+#ifdef PASTAR_PHASE_TIMERS
     const bool bprof = (view.timing & 4) && timing && blockIdx.x == 0 && threadIdx.x == 0;
     unsigned long long bt0 = bprof ? device_clock() : 0, bt;
 #define BPHASE(k)                                     \
@@ -1077,6 +1081,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         ctl->body_ticks[k] += bt - bt0;               \
         bt0 = bt;                                     \
     }
+#else
+    constexpr bool bprof = false;
+#define BPHASE(k)
+#endif
     StepStats *st = a.stats;
     const int w = view.band_log2, f0 = view.f0;
     const int bound = *(volatile int *)a.goal_g;
@@ -1666,7 +1674,7 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
                 continue;
             pos[i] -= 1;
             const uint64_t dec = 1ull << P.kshift[i];
-            const int w = P.kword[i];
+            const int w = KW == 1 ? 0 : P.kword[i];
 #pragma unroll
             for (int k = 0; k < KW; k++)
                 if (w == k)
