@@ -916,11 +916,13 @@ int estimate_band_log2(pastar_ctx *c, int h0, int64_t band_opt, int *w_out)
         int64_t sum = 0;
         for (int64_t k = 0; k < cnt; k++)
             sum += (int64_t)kids[(size_t)k].f - h0;
-        // an eighth of the mean f increase of the origin's children: the
-        // best or tied-best width on every workload (profiles/r1_tune_*.txt:
-        // kinase 30 -> 21 ms, syn4x200 1.9 -> 1.5 ms with fewer expansions,
-        // PF08184 61 expansions for 60 serial, syn8x400 equal)
-        band = cnt ? std::max<int64_t>(1, sum / cnt / 8) : 1;
+        // an eighth of the mean f increase of the origin's children up to
+        // N = 6, a quarter beyond: the best or tied-best width on every
+        // workload (profiles/r1_tune_*.txt: kinase 30 -> 21 ms, syn4x200
+        // 1.9 -> 1.5 ms with fewer expansions, PF08184 61 expansions for 60
+        // serial; syn8x400 tied at 1/8 and 1/4, syn8x100 24.5 ms at 1/4
+        // against 29 at 1/8)
+        band = cnt ? std::max<int64_t>(1, sum / cnt / (c->n >= 7 ? 4 : 8)) : 1;
     }
     int w = 0;
     while ((2ll << w) <= band * 4 / 3 && w < 24)  // nearest power of two
