@@ -51,6 +51,13 @@ __device__ __forceinline__ int from_lane_above(int v)
     return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
 }
 
+// as from_lane_above, lane 63 receiving kPaInf (the row below the table)
+constexpr int kPaInf = 0x3fffffff;
+__device__ __forceinline__ int from_lane_above_inf(int v)
+{
+    return __builtin_amdgcn_update_dpp(kPaInf, v, 0x130, 0xf, 0xf, false);
+}
+
 __host__ __device__ constexpr size_t pairalign_lds_bytes(int maxl2, int alpha, bool sub_lds)
 {
     return (size_t)kPaWaves * (maxl2 + 1) * 5 + (size_t)(maxl2 + 1) + (sub_lds ? (size_t)alpha * alpha * 4 : 0) +
@@ -126,8 +133,11 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
         volatile int *my_progress = progress + band % kPaWaves;
         int32_t *Mrow = M + (int64_t)(row_ok ? i : 0) * W;
         int2 *Crow = C + (int64_t)(row_ok ? i : 0) * W;
-        int m = 0, a = kNoGap;          // this lane's cell of the previous step: (i, j + 1)
-        int down = 0, adown = kNoGap;   // (i + 1, j)
+        // EQ_GAPS: the cells past the last row and column are +inf, so the
+        // plain recurrence reproduces the borders (PairAlign.cpp:142-160:
+        // +30 per step from the corner) and only the corner is seeded
+        int m = EQ_GAPS ? kPaInf : 0, a = kNoGap;        // this lane's cell of the previous step: (i, j + 1)
+        int down = EQ_GAPS ? kPaInf : 0, adown = kNoGap;  // (i + 1, j)
         int diag = 0;                   // (i + 1, j + 1)
         int j = L2 + 63 - lane;         // column of step t: L2 - (t - (63 - lane))
         int cost = (j >= 0 && j <= L2) ? crow[s2[j]] : 0;  // one step ahead
@@ -169,27 +179,40 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 // only cells inside the table are kept.  Steps past the sweep
                 // (t >= nsteps) have j < 0 on every lane and change nothing.
                 const bool in = row_ok && j >= 0 && j <= L2;
-                const int m_up = from_lane_above(m), a_up = EQ_GAPS ? 0 : from_lane_above(a);
-                diag = down;
-                down = use_lds_below ? lb[u] : m_up;
-                adown = EQ_GAPS ? 0 : (use_lds_below ? lbd[u] : a_up);
+                int mm, aa = kNoGap;
                 const int cost_here = cost;
                 cost = nc[u];
-                const int right = m, aright = a;
-                const int c0 = down + (EQ_GAPS ? GO : (adown == kGapX ? GE : GO));
-                const int c1 = right + (EQ_GAPS ? GO : (aright == kGapY ? GE : GO));
-                int mm = c0 < c1 ? c0 : c1;
-                int aa = c0 < c1 ? kGapX : kGapY;
-                const int c2 = diag + cost_here;
-                aa = c2 < mm ? kNoGap : aa;
-                mm = c2 < mm ? c2 : mm;
-                const bool last_col = j == L2;
-                // borders (PairAlign.cpp:142-160)
-                const int m_lastcol = row_above_last ? GO : down + GE;
-                const int m_lastrow = (j == L2 - 1) ? GO : right + GE;
-                mm = last_row ? (last_col ? 0 : m_lastrow) : (last_col ? m_lastcol : mm);
-                aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
-                cb[u] = make_int2(mm * wgt, cost_here * wgt);
+                if constexpr (EQ_GAPS) {
+                    const int m_up = from_lane_above_inf(m);
+                    diag = down;
+                    down = use_lds_below ? lb[u] : m_up;
+                    const int right = m;
+                    mm = (down < right ? down : right) + GO;
+                    const int c2 = diag + cost_here;
+                    mm = c2 < mm ? c2 : mm;
+                    mm = (last_row && t0 + u == 0) ? 0 : mm;  // the corner (L1, L2)
+                } else {
+                    const int m_up = from_lane_above(m), a_up = from_lane_above(a);
+                    diag = down;
+                    down = use_lds_below ? lb[u] : m_up;
+                    adown = use_lds_below ? lbd[u] : a_up;
+                    const int right = m, aright = a;
+                    const int c0 = down + (adown == kGapX ? GE : GO);
+                    const int c1 = right + (aright == kGapY ? GE : GO);
+                    mm = c0 < c1 ? c0 : c1;
+                    aa = c0 < c1 ? kGapX : kGapY;
+                    const int c2 = diag + cost_here;
+                    aa = c2 < mm ? kNoGap : aa;
+                    mm = c2 < mm ? c2 : mm;
+                    const bool last_col = j == L2;
+                    // borders (PairAlign.cpp:142-160)
+                    const int m_lastcol = row_above_last ? GO : down + GE;
+                    const int m_lastrow = (j == L2 - 1) ? GO : right + GE;
+                    mm = last_row ? (last_col ? 0 : m_lastrow) : (last_col ? m_lastcol : mm);
+                    aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
+                }
+                // unsigned: cells outside the table may hold +inf, never stored
+                cb[u] = make_int2((int)((unsigned)mm * (unsigned)wgt), cost_here * wgt);
                 m = in ? mm : m;
                 a = EQ_GAPS ? 0 : (in ? aa : a);
                 tb[u] = m;
