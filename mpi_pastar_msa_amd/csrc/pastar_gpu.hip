@@ -275,6 +275,7 @@ struct pastar_ctx {
     DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
     Ctl *h_ctl = nullptr;                 // pinned
     bool searched = false;
+    bool walk_ready = false;  // one shard: the search already walked the goal's chain (h_walk_masks, h_walk info)
     int64_t score = -1;
     // capacities of the current search buffers (reused across searches)
     unsigned long long cap_kmax = 0, cap_pool = 0, cap_maxch = 0, cap_outbox = 0;
@@ -931,6 +932,45 @@ int estimate_band_log2(pastar_ctx *c, int h0, int64_t band_opt, int *w_out)
     return PASTAR_OK;
 }
 
+// Backtrace walk buffers (device and pinned host), allocated once per
+// context and grown with the path length.
+int ensure_walk_buffers(pastar_ctx *c, int total_len)
+{
+    if (!c->walk_key.p)
+        PA_TRY(c->walk_key.alloc(4));
+    if (!c->walk_last.p)
+        PA_TRY(c->walk_last.alloc(4));
+    if (!c->walk_info.p)
+        PA_TRY(c->walk_info.alloc(2));
+    if (c->walk_masks.n < (size_t)total_len + 1)
+        PA_TRY(c->walk_masks.alloc((size_t)total_len + 1));
+    if (!c->h_walk)
+        HIP_TRY(hipHostMalloc((void **)&c->h_walk, 64, hipHostMallocDefault));
+    if (c->h_walk_masks_n < (size_t)total_len + 1) {
+        if (c->h_walk_masks)
+            (void)hipHostFree(c->h_walk_masks);
+        c->h_walk_masks = nullptr;
+        c->h_walk_masks_n = 0;
+        HIP_TRY(hipHostMalloc((void **)&c->h_walk_masks, 4 * ((size_t)total_len + 1), hipHostMallocDefault));
+        c->h_walk_masks_n = (size_t)total_len + 1;
+    }
+    return PASTAR_OK;
+}
+
+// Enqueue one walk stretch from coordinate pos (stream-ordered; the caller
+// synchronizes): key upload, walk kernel, info and masks back to pinned host
+// memory (h_walk[4..5] and h_walk_masks).
+int enqueue_walk(pastar_ctx *c, const uint16_t *pos, int total_len, bool local_only)
+{
+    const Ops ops = ops_for(c);
+    pack_key(c, pos, c->h_walk);
+    HIP_TRY(hipMemcpyAsync(c->walk_key.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+    ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_key.p, total_len + 1, local_only ? 1 : 0,
+             c->walk_masks.p, c->walk_last.p, c->walk_info.p);
+    PA_TRY(check_launch());
+    return PASTAR_OK;
+}
+
 template <int KWv>
 int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
 {
@@ -1253,6 +1293,23 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     PA_TRY(check_launch());
     HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
+    c->walk_ready = false;
+    if (G == 1) {
+        // the backtrace walk rides on this round trip: pastar_gpu_alignment
+        // then needs no launch and no wait of its own
+        int total_len = 0;
+        uint16_t goal_pos[PASTAR_MAX_SEQ] = {0};
+        for (int i = 0; i < c->n; i++) {
+            total_len += c->hp.len[i];
+            goal_pos[i] = (uint16_t)c->hp.len[i];
+        }
+        PA_TRY(ensure_walk_buffers(c, total_len));
+        PA_TRY(enqueue_walk(c, goal_pos, total_len, false));
+        HIP_TRY(hipMemcpyAsync(c->h_walk + 4, c->walk_info.p, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_walk_masks, c->walk_masks.p, 4 * ((size_t)total_len + 1), hipMemcpyDeviceToHost,
+                               c->stream));
+        c->walk_ready = true;
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     int goal_g = *h_goal_end;
     if (G > 1) {
@@ -1329,6 +1386,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
 {
     if (!c || !res)
         return fail(PASTAR_EINVAL, "null argument");
+    c->walk_ready = false;
     if (!c->heuristic_ready)
         return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
     HIP_TRY(hipSetDevice(c->device));
@@ -1466,20 +1524,9 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
         total_len += c->hp.len[i];
     if (stride < total_len + 1)
         return fail(PASTAR_EINVAL, "stride %d < %d", stride, total_len + 1);
-    const Ops ops = ops_for(c);
     // walk buffers live on the context (allocated once, grown with the
     // path length): a backtrace costs no allocation
-    if (!c->walk_key.p)
-        PA_TRY(c->walk_key.alloc(4));
-    if (!c->walk_last.p)
-        PA_TRY(c->walk_last.alloc(4));
-    if (!c->walk_info.p)
-        PA_TRY(c->walk_info.alloc(2));
-    if (c->walk_masks.n < (size_t)total_len + 1)
-        PA_TRY(c->walk_masks.alloc((size_t)total_len + 1));
-    if (!c->h_walk)
-        HIP_TRY(hipHostMalloc((void **)&c->h_walk, 64, hipHostMallocDefault));
-    uint64_t *dkey = c->walk_key.p, *dlast = c->walk_last.p;
+    PA_TRY(ensure_walk_buffers(c, total_len));
     int32_t *dmasks = c->walk_masks.p;
     int *dinfo = c->walk_info.p;
     int *h_info = reinterpret_cast<int *>(c->h_walk + 4);  // pinned: h_walk[0..3] is the key
@@ -1500,29 +1547,20 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
         // one host round trip per hop: the owner walks its stretch of the
         // chain, and with several shards the stretch (status, length, masks:
         // a fixed-size copy, so nobody needs the length first) goes to all
-        if (owner == c->shard) {
-            pack_key(c, pos.data(), c->h_walk);
-            HIP_TRY(hipMemcpyAsync(dkey, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
-            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, dkey, total_len + 1, G > 1 ? 1 : 0, dmasks,
-                     dlast, dinfo);
-            PA_TRY(check_launch());
+        if (G == 1 && guard == 0 && c->walk_ready) {
+            // walked at the end of the search, results already on the host
+        } else {
+            if (owner == c->shard)
+                PA_TRY(enqueue_walk(c, pos.data(), total_len, G > 1));
+            if (G > 1) {
+                PA_TRY(c->tr->broadcast(c, dinfo, 8, owner));
+                PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)(total_len + 1), owner));
+            }
+            HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->h_walk_masks, dmasks, 4 * ((size_t)total_len + 1), hipMemcpyDeviceToHost,
+                                   c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
         }
-        if (G > 1) {
-            PA_TRY(c->tr->broadcast(c, dinfo, 8, owner));
-            PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)(total_len + 1), owner));
-        }
-        HIP_TRY(hipMemcpyAsync(h_info, dinfo, 8, hipMemcpyDeviceToHost, c->stream));
-        if (c->h_walk_masks_n < (size_t)total_len + 1) {
-            if (c->h_walk_masks)
-                (void)hipHostFree(c->h_walk_masks);
-            c->h_walk_masks = nullptr;
-            c->h_walk_masks_n = 0;
-            HIP_TRY(hipHostMalloc((void **)&c->h_walk_masks, 4 * ((size_t)total_len + 1), hipHostMallocDefault));
-            c->h_walk_masks_n = (size_t)total_len + 1;
-        }
-        HIP_TRY(hipMemcpyAsync(c->h_walk_masks, dmasks, 4 * ((size_t)total_len + 1), hipMemcpyDeviceToHost,
-                               c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
         const int info[2] = {h_info[0], h_info[1]};
         if (info[1] < 0 || info[1] == 2)
             return fail(PASTAR_ENOTFOUND, "backtrace broken at step %d (status %d, shard %d)", info[0], info[1], owner);
