@@ -1420,9 +1420,9 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     if (o.depth < 0 || o.depth > 64)
         return fail(PASTAR_EINVAL, "depth %d outside [0, 64]", o.depth);
     // levels per launch: the cheaper an expansion, the deeper (PF08184 0.40
-    // -> 0.25 ms at 24; syn4x200 1.52 -> 1.44 ms at 12 with one round;
-    // profiles/r1_depth_sweep.txt)
-    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 24 : c->n == 4 ? 12 : 8);
+    // -> 0.22 ms at 64, 2 launches; syn4x200 1.52 -> 1.44 ms at 12 with one
+    // round; profiles/r1_depth_sweep.txt)
+    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 64 : c->n == 4 ? 12 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     int rc = PASTAR_OK, retries = 0;
