@@ -899,7 +899,9 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
             ctl->has_work = 0;
             const long long steps = ctl->steps + 1;
             ctl->steps = steps;
-            int status = ctl->n_shards == 1 ? 1 : 0;
+            // one shard: done; the sharded protocol decides on the host
+            // from every shard's has_work
+            int status = ctl->fuse ? 1 : 0;
             if (ctl->max_steps && steps >= ctl->max_steps && !status)
                 status = 3;
             if (status)
@@ -1533,7 +1535,7 @@ __global__ void step_pack_kernel(SearchArgs a, unsigned long long outbox_cap, in
     }
     out[G] = *a.goal_g;
     out[G + 1] = ctl->has_work;
-    out[G + 2] = ctl->status ? 1 : 0;
+    out[G + 2] = ctl->status >= 2 ? 1 : 0;  // capacity exhausted or step limit
 }
 
 // Reset the open list between searches: zero the chunk-table entries the

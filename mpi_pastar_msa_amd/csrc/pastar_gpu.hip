@@ -243,7 +243,9 @@ class RcclTransport : public Transport {
 
 struct pastar_ctx {
     int device = 0, n_shards = 1, shard = 0;
-    std::unique_ptr<Transport> tr;  // set when n_shards > 1
+    // set when the search runs the sharded protocol: n_shards > 1, or one
+    // shard with an RCCL communicator of its own (the protocol at world 1)
+    std::unique_ptr<Transport> tr;
     DevBuf<int64_t> xred;           // RCCL staging of small collectives
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -617,7 +619,7 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
     PA_TRY(setup_problem(c.get(), p));
-    if (n_shards > 1) {
+    if (n_shards > 1 || rccl_id) {
         if (!rccl_id)
             return fail(PASTAR_EINVAL, "rccl_id required for n_shards > 1");
         ncclUniqueId id;
@@ -857,7 +859,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         PA_TRY(c->ctl.alloc(1));
         PA_TRY(c->stamps.alloc(kArrive));
         PA_TRY(c->goal.alloc(1));
-        if (c->n_shards > 1) {
+        if (c->tr) {
             const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
             PA_TRY(c->outbox.alloc(bytes));
             PA_TRY(c->inbox.alloc(bytes));
@@ -1018,7 +1020,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         const char *e = std::getenv("PASTAR_TIMING_MASK");
         hc.timing = e && *e ? std::atoi(e) : 1;
     }
-    hc.fuse = G == 1 ? 1 : 0;  // one shard: select runs in the tail of expand
+    const bool sharded = c->tr != nullptr;  // the step protocol with an exchange
+    hc.fuse = sharded ? 0 : 1;  // one shard: select runs in the tail of expand
     hc.depth = cfg.depth;
     {
         const char *e = std::getenv("PASTAR_DEBUG");
@@ -1098,14 +1101,15 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
         PA_TRY(check_launch());
     }
-    if (G > 1)
+    if (sharded)
         HIP_TRY(hipStreamSynchronize(c->stream));
 
     double expand_ms = 0;
     int64_t launches = 0, exchanged = 0;
     Ctl h{};
+    c->graph_used = false;
     const double t0 = now_s();
-    if (G == 1) {
+    if (!sharded) {
         // one launch per step: expand the batch, and the last block to
         // finish cuts the next one (the first launch, with an empty batch,
         // only selects).  Runs of S steps are captured once and replayed
@@ -1117,7 +1121,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // context predicts, so few launches run after termination (each
         // would only read `status` and leave)
         constexpr int kLong = 32, kShort = 4;
-        c->graph_used = false;
         auto enqueue_steps = [&](int S) -> hipError_t {
             for (int k = 0; k < S; k++)
                 ops.expand(expand_grid, blk, c->stream, a);
@@ -1294,7 +1297,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
     c->walk_ready = false;
-    if (G == 1) {
+    if (!sharded) {
         // the backtrace walk rides on this round trip: pastar_gpu_alignment
         // then needs no launch and no wait of its own
         int total_len = 0;
@@ -1312,7 +1315,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     int goal_g = *h_goal_end;
-    if (G > 1) {
+    if (sharded) {
         int64_t mn[1] = {goal_g};
         PA_TRY(allreduce_i64(c, mn, 1, kRedMin));
         goal_g = (int)mn[0];
@@ -1369,7 +1372,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     res->expand_launches = launches;
     res->expand_parents = (int64_t)h.parents;
     int64_t all[1] = {(int64_t)h.expanded};
-    if (G > 1)
+    if (sharded)
         PA_TRY(allreduce_i64(c, all, 1, kRedSum));
     // the goal's acceptance counts as one expansion (PAStar.cpp:341)
     res->expansions_all = all[0] + 1;
@@ -1386,7 +1389,11 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
 {
     if (!c || !res)
         return fail(PASTAR_EINVAL, "null argument");
+    // a failed search must not leave an earlier search's result readable
+    // (the node table then holds this search's partial state)
     c->walk_ready = false;
+    c->searched = false;
+    c->score = -1;
     if (!c->heuristic_ready)
         return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
     HIP_TRY(hipSetDevice(c->device));
@@ -1437,7 +1444,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         if (rc != PASTAR_ENOMEM || o.no_autogrow || retries >= 8)
             break;
         int mask = c->last_fail_mask;
-        if (c->n_shards > 1) {  // every shard grows the same way
+        if (c->tr) {  // every shard grows the same way
             int64_t bits[4] = {mask & 1, (mask >> 1) & 1, (mask >> 2) & 1, (mask >> 3) & 1};
             const std::string err = g_err;
             if (allreduce_i64(c, bits, 4, kRedSum) != PASTAR_OK)
@@ -1547,12 +1554,12 @@ int pastar_gpu_alignment(pastar_ctx *c, char *rows, int stride, int *cols)
         // one host round trip per hop: the owner walks its stretch of the
         // chain, and with several shards the stretch (status, length, masks:
         // a fixed-size copy, so nobody needs the length first) goes to all
-        if (G == 1 && guard == 0 && c->walk_ready) {
+        if (guard == 0 && c->walk_ready) {
             // walked at the end of the search, results already on the host
         } else {
             if (owner == c->shard)
                 PA_TRY(enqueue_walk(c, pos.data(), total_len, G > 1));
-            if (G > 1) {
+            if (c->tr) {
                 PA_TRY(c->tr->broadcast(c, dinfo, 8, owner));
                 PA_TRY(c->tr->broadcast(c, dmasks, 4 * (size_t)(total_len + 1), owner));
             }
@@ -1742,7 +1749,7 @@ int pastar_gpu_allreduce(pastar_ctx *c, int64_t *vals, int count, int op)
 {
     if (!c || !vals || count < 0 || count > 8 || op < 0 || op > 2)
         return fail(PASTAR_EINVAL, "invalid allreduce arguments");
-    if (!c->tr || c->n_shards == 1)
+    if (!c->tr)
         return PASTAR_OK;
     HIP_TRY(hipSetDevice(c->device));
     return c->tr->allreduce(c, vals, count, (RedOp)op);

@@ -121,6 +121,7 @@ orc_problem *orc_load_fasta(const char *path)
     if (!f)
         return NULL;
     orc_problem *p = (orc_problem *)calloc(1, sizeof(orc_problem));
+    orc_set_gaps(p, GAP_OPEN, GAP_EXT, GAP_GAP);
     size_t cap = 1 << 16, n = 0;
     char *cur = (char *)malloc(cap);
     char *line = NULL;
@@ -160,9 +161,17 @@ orc_problem *orc_from_seqs(int n, const char *const *seqs)
     if (n < 2 || n > ORC_MAX_SEQ)
         return NULL;
     orc_problem *p = (orc_problem *)calloc(1, sizeof(orc_problem));
+    orc_set_gaps(p, GAP_OPEN, GAP_EXT, GAP_GAP);
     for (int i = 0; i < n; i++)
         add_seq(p, seqs[i], (int)strlen(seqs[i]));
     return p;
+}
+
+void orc_set_gaps(orc_problem *p, int gap_open, int gap_ext, int gap_gap)
+{
+    p->gap_open = gap_open;
+    p->gap_ext = gap_ext;
+    p->gap_gap = gap_gap;
 }
 
 void orc_free(orc_problem *p)
@@ -588,7 +597,7 @@ int orc_init_heuristic(orc_problem *p)
             p->pair_x[k] = i;
             p->pair_y[k] = j;
             p->H[k] = (int *)malloc(sizeof(int) * (size_t)(p->len[i] + 1) * (p->len[j] + 1));
-            orc_pairalign(p->seq[i], p->len[i], p->seq[j], p->len[j], GAP_OPEN, GAP_EXT, p->H[k]);
+            orc_pairalign(p->seq[i], p->len[i], p->seq[j], p->len[j], p->gap_open, p->gap_ext, p->H[k]);
         }
     p->npairs = k;
     float *w = (float *)malloc(sizeof(float) * (size_t)n * n);
@@ -675,7 +684,7 @@ void orc_initial_node(const orc_problem *p, orc_node *out)
 }
 
 /* Node::pairCost, Node.cpp:130-152 */
-static int pair_cost(int m, int mm, int s1, int s2, int parenti)
+static int pair_cost(const orc_problem *p, int m, int mm, int s1, int s2, int parenti)
 {
     int b1 = (m >> s1) & 1, b2 = (m >> s2) & 1, s;
     if (b1 && b2)
@@ -685,10 +694,10 @@ static int pair_cost(int m, int mm, int s1, int s2, int parenti)
     else if (b2)
         s = s1;
     else
-        return GAP_GAP;
+        return p->gap_gap;
     if (((parenti >> s) & 1) != ((m >> s) & 1))
-        return GAP_OPEN;
-    return GAP_EXT;
+        return p->gap_open;
+    return p->gap_ext;
 }
 
 int orc_get_neigh(const orc_problem *p, const orc_node *in, int vec_size,
@@ -714,7 +723,7 @@ int orc_get_neigh(const orc_problem *p, const orc_node *in, int vec_size,
             continue;
         int costs = 0;
         for (int k = 0; k < np; k++)
-            costs += pair_cost(m, mm[k], p->pair_x[k], p->pair_y[k], in->parenti) * p->weight[k];
+            costs += pair_cost(p, m, mm[k], p->pair_x[k], p->pair_y[k], in->parenti) * p->weight[k];
         c.g = in->g + costs;
         c.f = c.g + orc_h(p, c.pos);
         c.parenti = m;
@@ -1059,7 +1068,7 @@ int64_t orc_alignment_cost(const orc_problem *p, const char *aln, int stride, in
         for (int k = 0; k < p->npairs; k++) {
             int x = p->pair_x[k], y = p->pair_y[k];
             int mm = cost_c(p->seq[x][pos[x]], p->seq[y][pos[y]]);
-            g += (int64_t)pair_cost(m, mm, x, y, parenti) * p->weight[k];
+            g += (int64_t)pair_cost(p, m, mm, x, y, parenti) * p->weight[k];
         }
         for (int i = 0; i < n; i++)
             pos[i] = (uint16_t)(pos[i] + ((m >> i) & 1));

@@ -32,6 +32,8 @@ typedef struct orc_problem {
     int pair_x[ORC_MAX_PAIRS], pair_y[ORC_MAX_PAIRS];
     int npairs;
     int *H[ORC_MAX_PAIRS];          /* PairAlign suffix tables, row-major   */
+    int gap_open, gap_ext, gap_gap; /* Cost.h:13 (all 30); patchable so the
+                                       general pairCost form can be checked */
 } orc_problem;
 
 typedef struct orc_node {
@@ -57,6 +59,9 @@ int orc_cost(int r, int l);
 orc_problem *orc_load_fasta(const char *path);
 orc_problem *orc_from_seqs(int n, const char *const *seqs);
 void orc_free(orc_problem *p);
+
+/* Patch the gap constants (Cost.h:13) before orc_init_heuristic. */
+void orc_set_gaps(orc_problem *p, int gap_open, int gap_ext, int gap_gap);
 
 /* Phase 1: HeuristicHPair::init (HeuristicHPair.cpp:47-67). */
 int orc_init_heuristic(orc_problem *p);

@@ -25,6 +25,9 @@ class orc_problem(ctypes.Structure):
         ("pair_y", ctypes.c_int * MAX_PAIRS),
         ("npairs", ctypes.c_int),
         ("H", ctypes.POINTER(ctypes.c_int) * MAX_PAIRS),
+        ("gap_open", ctypes.c_int),
+        ("gap_ext", ctypes.c_int),
+        ("gap_gap", ctypes.c_int),
     ]
 
 
@@ -55,6 +58,7 @@ def lib():
         L.orc_from_seqs.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
         L.orc_free.argtypes = [P]
         L.orc_init_heuristic.argtypes = [P]
+        L.orc_set_gaps.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_h.argtypes = [P, ctypes.POINTER(ctypes.c_uint16)]
         L.orc_get_id.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint16), ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int]
@@ -76,7 +80,8 @@ def lib():
 class Oracle:
     """One problem instance of the CPU oracle."""
 
-    def __init__(self, fasta=None, seqs=None):
+    def __init__(self, fasta=None, seqs=None, gaps=None):
+        """gaps: (gap_open, gap_ext, gap_gap) patched over Cost.h:13's 30s."""
         L = lib()
         if fasta is not None:
             self.p = L.orc_load_fasta(str(fasta).encode())
@@ -85,6 +90,8 @@ class Oracle:
             self.p = L.orc_from_seqs(len(seqs), arr)
         if not self.p:
             raise OSError("oracle could not load the input")
+        if gaps is not None:
+            L.orc_set_gaps(self.p, *gaps)
         if L.orc_init_heuristic(self.p) != 0:
             raise ValueError("oracle init failed")
         pr = self.p.contents

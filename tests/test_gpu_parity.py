@@ -286,3 +286,122 @@ def test_cli_hash_options():
     assert r.returncode == 0, r.stderr
     assert any("Partial-Sum hash, 5 shift." in l for l in r.stdout.splitlines()), r.stdout
     assert "g - 45037 (h - 0 f - 45037)" in r.stdout
+
+
+# ---------------------------------------------------------------------------
+# Round 2: the BASELINE configs not covered before, the general gap form of g,
+# state after a failed search, and the RCCL transport at world size 1.
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("gaps", [(35, 25, 30), (20, 40, 10)])
+@pytest.mark.parametrize("name", ["test2", "PF08184", "syn4x200_s1", "kinase"])
+def test_get_neigh_general_gap_form(name, gaps, kat):
+    """Node::pairCost's open / extend / gap-gap branches (Node.cpp:130-152)
+    with patched constants: g (and h, whose PairAlign tables use the same
+    patched open / extension costs) of every neighbour of random parents,
+    against the oracle's getNeigh under the same constants."""
+    go, ge, gg = gaps
+    ref = kat["inputs"][name]
+    o = orc.Oracle(fasta=golden(ref["file"]), gaps=gaps)
+    rng = random.Random(zlib.crc32(("gap/%s/%d/%d/%d" % (name, go, ge, gg)).encode()))
+    nodes = _random_nodes(o, 150, rng)
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    with Engine(seqs, gap_open=go, gap_ext=ge, gap_gap=gg).init() as e:
+        from mpi_pastar_msa_amd.pastar import Node
+        kids, owner, src = e.get_neigh_batch([Node(*nd) for nd in nodes], 8)
+        got = {}
+        for k, ow, s in zip(kids, owner, src):
+            got.setdefault(s, []).append(((k.pos, k.g, k.f, k.parenti), ow))
+        for s, nd in enumerate(nodes):
+            assert got.get(s, []) == o.get_neigh(nd, 8), (s, nd)
+        # the parent's own last move decides open vs extend: the same
+        # coordinate under every parent mask
+        pos = tuple(L // 2 for L in o.lengths)
+        for pm in range(1, 1 << o.n):
+            nd = (pos, 1000, 1000 + o.h(pos), pm)
+            kids, owner, _ = e.get_neigh_batch([Node(*nd)], 1)
+            assert [((k.pos, k.g, k.f, k.parenti), w) for k, w in zip(kids, owner)] == o.get_neigh(nd, 1)
+
+
+def test_search_syn8x400_s5(kat):
+    """configs[4]'s workload (8 x 400, 255 neighbours per expansion) at one
+    GPU: the optimal score the reference reached at -t 8 and a valid optimal
+    alignment."""
+    ref = kat["inputs"]["syn8x400_s5"]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    with Engine(seqs).init() as e:
+        assert e.weight_matrix == o.weights
+        r = e.pa_star(PAStarOpt())
+        assert r.score == ref["score"] == 1318889
+        rows = e.alignment()
+        assert [row.replace("-", "") for row in rows] == seqs.seqs
+        assert o.alignment_cost(rows) == ref["score"]
+
+
+@pytest.mark.parametrize("name,shards,hash_type,shift", [("kinase", 8, "FZORDER", 12),
+                                                          ("syn8x400_s5", 8, "FZORDER", 12)])
+def test_sharded_search_baseline_configs(name, shards, hash_type, shift, kat):
+    """configs[3] (kinase, CoordHash z-order partition over 8 shards) and
+    configs[4] (syn8x400 over 8 shards) through the sharded protocol with
+    the in-process shard group on one GPU: exact score, a valid optimal
+    alignment (md5 where the reference pins it), expansions and exchange
+    accounted on every shard."""
+    from mpi_pastar_msa_amd import sharded_search
+    ref = kat["inputs"][name]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    res, rows = sharded_search(seqs, shards, hash_type=hash_type, hash_shift=shift)
+    assert [r.score for r in res] == [ref["score"]] * shards
+    assert sum(r.expansions for r in res) + 1 == res[0].expansions_all
+    assert all(r.expansions > 0 for r in res)  # the z-order partition spreads the work
+    assert sum(r.exchanged for r in res) > 0
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    assert o.alignment_cost(rows) == ref["score"]
+    if "alignment_md5" in ref:
+        assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
+def test_failed_search_invalidates_previous_result(kat):
+    """A search that stops at the step limit leaves no readable result: the
+    node table holds its partial state, so the backtrace and the closed-list
+    lookup refuse (PASTAR_ESTATE) instead of walking it."""
+    from mpi_pastar_msa_amd._native import ESTATE, NativeError
+    ref = kat["inputs"]["syn4x200_s1"]
+    with _engine("syn4x200_s1", kat) as e:
+        assert e.pa_star(PAStarOpt()).score == ref["score"]
+        e.alignment()
+        with pytest.raises(NativeError) as ex:
+            e.pa_star(PAStarOpt(max_steps=2))
+        assert ex.value.code == ESTATE
+        for call in (e.alignment, lambda: e.closed_lookup(e.sequences.get_final_coord())):
+            with pytest.raises(NativeError) as ex:
+                call()
+            assert ex.value.code == ESTATE
+        # and a later successful search is readable again
+        assert e.pa_star(PAStarOpt()).score == ref["score"]
+        assert o_cost(kat, "syn4x200_s1", e.alignment()) == ref["score"]
+
+
+def o_cost(kat, name, rows):
+    return orc.Oracle(fasta=golden(kat["inputs"][name]["file"])).alignment_cost(rows)
+
+
+@pytest.mark.parametrize("name", ["test2", "syn4x200_s1", "kinase"])
+def test_rccl_transport_world_one(name, kat):
+    """The RCCL transport (RcclTransport: allgather of the step values,
+    grouped send/recv, allreduce, broadcast of the backtrace stretches) on a
+    one-rank communicator: the sharded step protocol end to end on one GPU,
+    same score and alignment as the one-shard engine."""
+    from mpi_pastar_msa_amd import rccl_unique_id
+    ref = kat["inputs"][name]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    with Engine(seqs, n_shards=1, shard_rank=0, rccl_id=rccl_unique_id()).init() as e:
+        r = e.pa_star(PAStarOpt())
+        assert r.score == ref["score"]
+        assert r.graph_replay == 0  # the sharded protocol: host-driven steps
+        assert e.allreduce([3, 5], "max") == [3, 5]
+        e.barrier()
+        rows = e.alignment()
+        assert o_cost(kat, name, rows) == ref["score"]
+        if "alignment_md5" in ref:
+            assert hashlib.md5("".join(x + "\n" for x in rows).encode()).hexdigest() == ref["alignment_md5"]

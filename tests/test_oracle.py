@@ -150,3 +150,20 @@ def test_alignment_cost_rejects_invalid(kat):
     o = orc.Oracle(fasta=golden("test2.fasta"))
     rows = o.astar()["rows"]
     assert o.alignment_cost([r[:-1] for r in rows]) == -1  # does not reach the goal
+
+
+def test_oracle_gap_constants_patchable(kat):
+    """The oracle's pairCost / PairAlign take patched gap constants (the
+    general form §8 a2 keeps): the reference's 30s reproduce the default
+    instance, other constants change g and h."""
+    f = golden(kat["inputs"]["test2"]["file"])
+    base, same = orc.Oracle(fasta=f), orc.Oracle(fasta=f, gaps=(30, 30, 30))
+    other = orc.Oracle(fasta=f, gaps=(35, 25, 10))
+    nd = base.initial_node()
+    assert same.get_neigh(nd) == base.get_neigh(nd)
+    assert same.h(nd[0]) == base.h(nd[0]) == kat["inputs"]["test2"]["h_origin"]
+    assert other.get_neigh(nd) != base.get_neigh(nd)
+    # with every move a gap-gap or an extension the costs follow the patch
+    kids = {k[3]: k for k, _ in other.get_neigh(((1,) * base.n, 0, 0, (1 << base.n) - 1))}
+    kb = {k[3]: k for k, _ in base.get_neigh(((1,) * base.n, 0, 0, (1 << base.n) - 1))}
+    assert kids.keys() == kb.keys()
