@@ -41,7 +41,7 @@ extern "C" {
 #endif
 
 #define PASTAR_MAX_SEQ 16
-#define PASTAR_ABI_VERSION 1
+#define PASTAR_ABI_VERSION 2
 
 /* status codes */
 #define PASTAR_OK 0
@@ -112,8 +112,19 @@ typedef struct pastar_search_opts {
                                  falls in the step's buckets are expanded by
                                  the same workgroup in the same launch, up to
                                  depth - 1 more levels (0 = default)       */
-    int32_t pad;
+    int32_t mode;             /* PASTAR_MODE_*: which engine runs the search */
 } pastar_search_opts;
+
+/* pastar_search_opts.mode */
+#define PASTAR_MODE_AUTO 0    /* the LDS-resident search when the problem fits
+                                 one workgroup's LDS (pair tables plus a node
+                                 table of >= 256 slots; equal gap costs,
+                                 one shard), else (or once it overflows) the
+                                 batched engine                             */
+#define PASTAR_MODE_BATCHED 1 /* the batched multi-workgroup engine only    */
+#define PASTAR_MODE_SOLO 2    /* the LDS-resident search only (PASTAR_EINVAL
+                                 if the problem does not fit, PASTAR_ENOMEM
+                                 if the search outgrows the node table)    */
 
 typedef struct pastar_result {
     int64_t score;          /* optimal weighted SP score (goal g)              */
@@ -139,6 +150,9 @@ typedef struct pastar_result {
     double gap_ms;          /* profile = 1, one shard: device idle between
                                the end of one step and the start of the next
                                (launch gaps)                               */
+    int64_t solo;           /* 1 when the search ran on the LDS-resident path
+                               (one launch: PairAlign, search, backtrace;
+                               steps = levels, expand_ms = that launch)    */
 } pastar_result;
 
 typedef struct pastar_ctx pastar_ctx;

@@ -54,7 +54,7 @@ class pastar_search_opts(ctypes.Structure):
         ("no_autogrow", ctypes.c_int32),
         ("eager", ctypes.c_int32),
         ("depth", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
+        ("mode", ctypes.c_int32),
     ]
 
 
@@ -81,6 +81,7 @@ class pastar_result(ctypes.Structure):
         ("graph_replay", ctypes.c_int64),
         ("select_ms", ctypes.c_double),
         ("gap_ms", ctypes.c_double),
+        ("solo", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -32,6 +32,7 @@
 #include "host_model.hpp"
 #include "kernels.hpp"
 #include "pastar_gpu.h"
+#include "solo.hpp"
 
 using namespace pastar;
 using namespace pastar::dev;
@@ -260,8 +261,19 @@ struct pastar_ctx {
     DevBuf<int2> dHC;
     DevBuf<uint8_t> dcodes;
     DevBuf<int32_t> dsub;
-    bool heuristic_ready = false;
+    bool heuristic_ready = false;  // pastar_gpu_build_heuristic called
+    bool hc_built = false;         // HC written in HBM (launched lazily: the LDS-resident search builds its own)
     bool plain_h_ready = false;  // H written (pastar_gpu_pair_table)
+    size_t codes_len = 0;
+    // LDS-resident search of small problems (solo.hpp)
+    bool solo_failed = false;  // a solo search of this problem overflowed its LDS capacity
+    bool solo_active = false;  // the last search ran on the solo path (its node table is solo_dump)
+    unsigned solo_attr_done = 0;  // per N: dynamic LDS limit raised
+    DevBuf<uint8_t> solo_buf;     // SoloOut + backtrace masks
+    DevBuf<uint64_t> solo_dump;   // the solo node table in the main slot layout
+    int solo_cap_log2 = 0;
+    unsigned char *h_solo = nullptr;  // pinned copy of solo_buf
+    size_t h_solo_n = 0;
 
     // search state
     DevBuf<uint64_t> table;
@@ -433,6 +445,7 @@ int setup_problem(pastar_ctx *c, const pastar_problem *p)
             hoff += (int64_t)(hp.len[x] + 1) * (hp.len[y] + 1);
         }
 
+    c->codes_len = codes.size();
     PA_TRY(c->dH.alloc((size_t)hoff));
     PA_TRY(c->dHC.alloc((size_t)hoff));
     PA_TRY(c->dcodes.alloc(codes.size()));
@@ -660,6 +673,8 @@ void pastar_gpu_destroy(pastar_ctx *c)
         (void)hipHostFree(c->h_gather);
     if (c->h_walk_masks)
         (void)hipHostFree(c->h_walk_masks);
+    if (c->h_solo)
+        (void)hipHostFree(c->h_solo);
     if (c->ev0)
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
@@ -708,14 +723,27 @@ static int launch_pairalign(pastar_ctx *c, bool write_h)
     return PASTAR_OK;
 }
 
+// The search form of the pair tables in HBM, built on first use.
+static int ensure_hc(pastar_ctx *c)
+{
+    if (c->hc_built)
+        return PASTAR_OK;
+    PA_TRY(launch_pairalign(c, false));
+    c->hc_built = true;
+    return PASTAR_OK;
+}
+
 int pastar_gpu_build_heuristic(pastar_ctx *c)
 {
     if (!c)
         return fail(PASTAR_EINVAL, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
-    // the search and h read only HC; H is written on demand (pair_table)
-    PA_TRY(launch_pairalign(c, false));
+    // the search and h read only HC; H is written on demand (pair_table).
+    // The wavefront launch itself is deferred to the first call that reads
+    // HC from HBM (ensure_hc): the LDS-resident search of a small problem
+    // runs PairAlign inside its own launch
     c->heuristic_ready = true;
+    c->hc_built = false;
     c->plain_h_ready = false;
     return PASTAR_OK;
 }
@@ -730,6 +758,7 @@ int pastar_gpu_pair_table(pastar_ctx *c, int pair, int32_t *out)
     if (!c->plain_h_ready) {
         PA_TRY(launch_pairalign(c, true));
         c->plain_h_ready = true;
+        c->hc_built = true;
     }
     const size_t cells = (size_t)(c->hp.len[c->hp.pair_x[pair]] + 1) * (c->hp.len[c->hp.pair_y[pair]] + 1);
     HIP_TRY(hipMemcpy(out, c->dH.p + c->hp.h_off[pair], cells * 4, hipMemcpyDeviceToHost));
@@ -757,6 +786,7 @@ int pastar_gpu_h(pastar_ctx *c, const uint16_t *pos, int count, int32_t *out)
             if (pos[(size_t)k * PASTAR_MAX_SEQ + i] > c->hp.len[i])
                 return fail(PASTAR_EINVAL, "coordinate %d outside the lattice", k);
     HIP_TRY(hipSetDevice(c->device));
+    PA_TRY(ensure_hc(c));
     DevBuf<uint16_t> dpos;
     DevBuf<int32_t> dout;
     PA_TRY(dpos.alloc((size_t)count * PASTAR_MAX_SEQ));
@@ -793,6 +823,7 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
         total += (1ll << free_dims) - 1;
     }
     HIP_TRY(hipSetDevice(c->device));
+    PA_TRY(ensure_hc(c));
     DevBuf<pastar_node> din, dout;
     DevBuf<int64_t> doff;
     DevBuf<int32_t> down, dsrc;
@@ -967,6 +998,8 @@ int enqueue_walk(pastar_ctx *c, const uint16_t *pos, int total_len, bool local_o
     const Ops ops = ops_for(c);
     pack_key(c, pos, c->h_walk);
     HIP_TRY(hipMemcpyAsync(c->walk_key.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+    if (c->solo_active)  // a solo search walks its own chain (solo.hpp)
+        return fail(PASTAR_ESTATE, "no node table walk after an LDS-resident search");
     ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_key.p, total_len + 1, local_only ? 1 : 0,
              c->walk_masks.p, c->walk_last.p, c->walk_info.p);
     PA_TRY(check_launch());
@@ -979,6 +1012,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     constexpr int KW = KWv;
     const Ops ops = ops_for(c);
     const int G = c->n_shards;
+    PA_TRY(ensure_hc(c));
+    c->solo_active = false;
     PA_TRY(alloc_search(c, cfg));
     const int lpn = std::min(64, 1 << c->n);
     const int per_block = kWaves * (64 / lpn);
@@ -1381,6 +1416,171 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     return PASTAR_OK;
 }
 
+// ---------------------------------------------------------------------------
+// LDS-resident search of a small problem (solo.hpp): PairAlign, the A* and
+// the backtrace in one single-workgroup launch.
+// ---------------------------------------------------------------------------
+struct SoloPlan {
+    SoloArgs a;
+    size_t lds;
+};
+
+// The LDS layout, or false when the problem does not take the solo path:
+// equal gap costs, 1-word keys, one shard, 2..8 sequences, and the pair
+// tables plus a node table of at least 2^kSoloMinCapLog2 slots in 160 KB.
+bool solo_plan(const pastar_ctx *c, SoloPlan *pl)
+{
+    if (c->tr || c->kw != 1 || c->n < 2 || c->n > 8 || c->hp.gap_open != c->hp.gap_ext)
+        return false;
+    if (c->hp.kshift[c->n - 1] + c->hp.kbits[c->n - 1] > kSoloKeyBits)
+        return false;  // coordinates in 31 bits (32-bit keys)
+    auto align16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+    size_t cells = 0;
+    for (int k = 0; k < c->npairs; k++)
+        cells += (size_t)(c->hp.len[c->hp.pair_x[k]] + 1) * (c->hp.len[c->hp.pair_y[k]] + 1);
+    SoloArgs &a = pl->a;
+    std::memset(&a, 0, sizeof(a));
+    size_t off = align16(cells * 8);
+    a.off_prob = (int)off;
+    off = align16(off + sizeof(DevProblem));
+    a.off_sub = (int)off;
+    off = align16(off + (size_t)c->hp.alpha * c->hp.alpha * 4);
+    a.off_codes = (int)off;
+    off = align16(off + c->codes_len);
+    if (off >= (size_t)kSoloLds)
+        return false;
+    int lg = kSoloMaxCapLog2;
+    while (lg >= kSoloMinCapLog2 && off + ((size_t)kSoloSlotBytes << lg) > (size_t)kSoloLds)
+        lg--;
+    if (lg < kSoloMinCapLog2)
+        return false;
+    const size_t C = (size_t)1 << lg;
+    a.off_best = (int)off;  // 8-B arrays first
+    a.off_hcl = (int)(off + 8 * C);
+    a.off_open = (int)(off + 16 * C);
+    a.off_batch = (int)(off + 24 * C);  // 2 x C/4 entries of 16 B
+    a.off_keys = (int)(off + 32 * C);   // 4-B keys last
+    a.cap_log2 = lg;
+    a.hc_cells = (int)cells;
+    a.codes_len = (int)c->codes_len;
+    a.alpha2 = c->hp.alpha * c->hp.alpha;
+    pl->lds = off + kSoloSlotBytes * C;
+    return true;
+}
+
+template <int N>
+const void *solo_fn()
+{
+    return (const void *)solo_kernel<N>;
+}
+
+const void *solo_fn_for(int n)
+{
+    switch (n) {
+    case 2: return solo_fn<2>();
+    case 3: return solo_fn<3>();
+    case 4: return solo_fn<4>();
+    case 5: return solo_fn<5>();
+    case 6: return solo_fn<6>();
+    case 7: return solo_fn<7>();
+    default: return solo_fn<8>();
+    }
+}
+
+// Returns PASTAR_ENOMEM when the search outgrew the LDS node table (the
+// caller then runs the batched engine).
+int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result *res)
+{
+    int total_len = 0;
+    for (int i = 0; i < c->n; i++)
+        total_len += c->hp.len[i];
+    const size_t out_bytes = sizeof(SoloOut) + 4 * ((size_t)total_len + 1);
+    if (c->solo_buf.n < out_bytes)
+        PA_TRY(c->solo_buf.alloc(out_bytes));
+    const size_t C = (size_t)1 << pl.a.cap_log2;
+    if (c->solo_dump.n < 4 * C)
+        PA_TRY(c->solo_dump.alloc(4 * C));
+    if (c->h_solo_n < out_bytes) {
+        if (c->h_solo)
+            (void)hipHostFree(c->h_solo);
+        c->h_solo = nullptr;
+        c->h_solo_n = 0;
+        HIP_TRY(hipHostMalloc((void **)&c->h_solo, out_bytes, hipHostMallocDefault));
+        c->h_solo_n = out_bytes;
+    }
+    PA_TRY(ensure_walk_buffers(c, total_len));
+    SoloArgs a = pl.a;
+    a.P = c->dP.p;
+    a.codes = c->dcodes.p;
+    a.sub = c->dsub.p;
+    a.out = reinterpret_cast<SoloOut *>(c->solo_buf.p);
+    a.masks = reinterpret_cast<int32_t *>(c->solo_buf.p + sizeof(SoloOut));
+    a.dump = c->solo_dump.p;
+    a.max_path = total_len + 1;
+    a.max_levels = cfg.max_steps > 0 ? cfg.max_steps : (1ll << 40);
+    a.band_log2 = -1;
+    if (cfg.band > 0) {
+        int w = 0;
+        PA_TRY(estimate_band_log2(c, 0, cfg.band, &w));
+        a.band_log2 = w;
+    }
+    const void *fn = solo_fn_for(c->n);
+    if (!(c->solo_attr_done & (1u << c->n))) {
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSoloLds));
+        c->solo_attr_done |= 1u << c->n;
+    }
+    void *args[] = {(void *)&a};
+    const double t0 = now_s();
+    HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(kSoloThreads), args, pl.lds, c->stream));
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemcpyAsync(c->h_solo, c->solo_buf.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const double t1 = now_s();
+    SoloOut o;
+    std::memcpy(&o, c->h_solo, sizeof(o));
+    if (cfg.verbose)
+        std::fprintf(stderr, "[pastar solo] status %d levels %d (%llu pile cuts) cap %d: tables %.2f us, search %.2f us, tail %.2f us\n",
+                     o.status, o.levels, o.pile_cuts, o.cap, (o.t_tables - o.t_start) * 1e-2, (o.t_search - o.t_tables) * 1e-2,
+                     (o.t_end - o.t_search) * 1e-2);
+    if (cfg.verbose && o.phase[0] + o.phase[1] + o.phase[2] + o.phase[3])
+        std::fprintf(stderr, "[pastar solo] per level (core clocks): top %.0f, entry+reads %.0f, children+relax %.0f, "
+                     "push+tail %.0f\n", (double)o.phase[0] / o.levels, (double)o.phase[1] / o.levels,
+                     (double)o.phase[2] / o.levels, (double)o.phase[3] / o.levels);
+    if (o.status == 2)
+        return fail(PASTAR_ENOMEM, "LDS-resident search outgrew its %d-slot node table", o.cap);
+    if (o.status == 4)
+        return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
+    if (o.status != 1 || o.score == kIntMax)
+        return fail(PASTAR_ENOTFOUND, "search exhausted without reaching the goal");
+    // the backtrace rides on the same copy (pastar_gpu_alignment reads it)
+    std::memcpy(c->h_walk_masks, c->h_solo + sizeof(SoloOut), 4 * (size_t)std::min(o.path_len, total_len + 1));
+    int *h_info = reinterpret_cast<int *>(c->h_walk + 4);
+    h_info[0] = o.path_len;
+    h_info[1] = o.path_status;
+    c->walk_ready = true;
+    c->solo_active = true;
+    c->solo_cap_log2 = pl.a.cap_log2;
+    std::memset(res, 0, sizeof(*res));
+    res->score = o.score;
+    res->expansions = (int64_t)o.expanded;
+    res->expansions_all = (int64_t)o.expanded + 1;  // the goal's acceptance (PAStar.cpp:341)
+    res->reopen = (int64_t)o.reopen;
+    res->generated = (int64_t)o.generated;
+    res->open_size = (int64_t)o.open_left;
+    res->closed_size = (int64_t)(o.expanded - o.reopen);
+    res->table_used = (int64_t)o.claimed;
+    res->steps = o.levels;
+    res->seconds = t1 - t0;
+    res->expand_ms = (double)(o.t_end - o.t_start) * 1e-5;
+    res->expand_launches = 1;
+    res->expand_parents = (int64_t)(o.expanded + o.dropped);
+    res->table_slots = (int64_t)C;
+    res->solo = 1;
+    c->searched = true;
+    c->score = o.score;
+    return PASTAR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1432,6 +1632,22 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 64 : c->n == 4 ? 12 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
+    if (o.mode < PASTAR_MODE_AUTO || o.mode > PASTAR_MODE_SOLO)
+        return fail(PASTAR_EINVAL, "search mode %d", o.mode);
+    // a small problem runs whole in one workgroup's LDS (solo.hpp); one that
+    // outgrows it runs on the batched engine from then on
+    {
+        SoloPlan pl;
+        const bool fits = solo_plan(c, &pl);
+        if (o.mode == PASTAR_MODE_SOLO && !fits)
+            return fail(PASTAR_EINVAL, "the problem does not fit the LDS-resident search");
+        if (fits && (o.mode == PASTAR_MODE_SOLO || (o.mode == PASTAR_MODE_AUTO && !c->solo_failed))) {
+            const int src = solo_search(c, cfg, pl, res);
+            if (src != PASTAR_ENOMEM || o.mode == PASTAR_MODE_SOLO)
+                return src;
+            c->solo_failed = true;
+        }
+    }
     int rc = PASTAR_OK, retries = 0;
     for (;;) {
         c->last_fail_mask = 0;
@@ -1504,7 +1720,13 @@ int pastar_gpu_closed_lookup(pastar_ctx *c, const uint16_t *pos, pastar_node *ou
     PA_TRY(dk.alloc(4));
     PA_TRY(dout.alloc(3));
     HIP_TRY(hipMemcpyAsync(dk.p, key, 32, hipMemcpyHostToDevice, c->stream));
-    ops_for(c).lookup(c->stream, c->table.p, c->nslots - 1, dk.p, dout.p);
+    // the node table of the last search: the main table, or the LDS-resident
+    // search's dump (same slot layout)
+    if (c->solo_active)
+        hipLaunchKernelGGL(solo_lookup_kernel, dim3(1), dim3(1), 0, c->stream, c->solo_dump.p, c->solo_cap_log2, dk.p,
+                           dout.p);
+    else
+        ops_for(c).lookup(c->stream, c->table.p, c->nslots - 1, dk.p, dout.p);
     PA_TRY(check_launch());
     uint64_t r[3];
     HIP_TRY(hipMemcpyAsync(r, dout.p, 24, hipMemcpyDeviceToHost, c->stream));

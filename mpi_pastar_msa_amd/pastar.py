@@ -128,12 +128,14 @@ class PAStarOpt:
     autogrow: bool = True
     eager: bool = False
     depth: int = 0
+    mode: str = "auto"  # "auto": LDS-resident search when the problem fits; "batched"; "solo"
 
     def search_opts(self):
         return nat.pastar_search_opts(self.batch_nodes, self.batch_min, self.table_slots_log2, self.pool_entries,
                                       self.subqueue_entries, self.max_steps, self.band, int(self.profile),
                                       int(self.verbose),
-                                      int(not self.autogrow), int(self.eager), int(self.depth), 0)
+                                      int(not self.autogrow), int(self.eager), int(self.depth),
+                                      {"auto": 0, "batched": 1, "solo": 2}[self.mode])
 
 
 def compute_weights(seqs):
@@ -175,6 +177,7 @@ class SearchResult:
     graph_replay: int = 0
     select_ms: float = 0.0
     gap_ms: float = 0.0
+    solo: int = 0
     extra: dict = field(default_factory=dict)
 
 

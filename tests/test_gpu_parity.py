@@ -100,8 +100,8 @@ def test_get_neigh_matches_oracle(name, vec_size, hash_type, shift, kat, oracles
 def test_search_score_bit_exact(name, batch, eager, kat, oracles):
     ref = kat["inputs"][name]
     with _engine(name, kat) as e:
-        r = e.pa_star(PAStarOpt(batch_nodes=batch, eager=eager, profile=True))
-        assert r.graph_replay == (0 if eager else 1)
+        r = e.pa_star(PAStarOpt(batch_nodes=batch, eager=eager, profile=True, mode="batched"))
+        assert r.graph_replay == (0 if eager else 1) and r.solo == 0
         assert r.expand_ms > 0
         assert r.score == ref["score"]
         rows = e.alignment()
@@ -140,7 +140,8 @@ def test_search_n8(name, kat):
         assert o.alignment_cost(rows) == ref["score"]
 
 
-def test_random_small_problems_match_oracle():
+@pytest.mark.parametrize("mode", ["batched", "auto"])
+def test_random_small_problems_match_oracle(mode):
     rng = random.Random(7)
     alphabet = "ACDEFGHIKLMNPQRSTVWYBZ"
     for trial in range(12):
@@ -150,13 +151,15 @@ def test_random_small_problems_match_oracle():
         ref = o.astar()
         with Engine(seqs).init() as e:
             assert e.weight_matrix == o.weights
-            r = e.pa_star(PAStarOpt(batch_nodes=rng.choice([1, 3, 16, 0])))
+            r = e.pa_star(PAStarOpt(batch_nodes=rng.choice([1, 3, 16, 0]), mode=mode))
             assert r.score == ref["score"], (seqs, r, ref)
+            assert r.solo == 0 or mode == "auto"
             rows = e.alignment()
             assert o.alignment_cost(rows) == ref["score"]
 
 
-def test_random_edge_problems_match_oracle():
+@pytest.mark.parametrize("mode", ["batched", "auto"])
+def test_random_edge_problems_match_oracle(mode):
     """Edge shapes: 7 and 8 sequences (the multi-round child loop with 1-word
     keys), ragged lengths (1 residue beside 40), and residues the reference
     costs 0 (B J O U X Z and lower case, Cost.cpp:10-262)."""
@@ -174,7 +177,7 @@ def test_random_edge_problems_match_oracle():
         ref = o.astar()
         with Engine(seqs).init() as e:
             assert e.weight_matrix == o.weights
-            r = e.pa_star(PAStarOpt())
+            r = e.pa_star(PAStarOpt(mode=mode))
             assert r.score == ref["score"], (seqs, r, ref)
             rows = e.alignment()
             assert o.alignment_cost(rows) == ref["score"]
