@@ -52,6 +52,9 @@ WORKLOADS = {  # name -> (fasta fixture, BASELINE.json config it stands for, kno
 # serial (-t 1) expansion counts of the reference, for the useful rate
 SERIAL_EXPANSIONS = {"syn4x200_s1": 22089, "PF08184": 60, "kinase": 4497279}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+# the reference's own PF08184 run at -t 1: 60 expansions in
+# about 0.11 s (its receiver's backoff sleeps floor the wall time)
+REF_PF08184_T1_S, REF_PF08184_T1_NODES = 0.11, 60
 
 
 def bytes_per_expansion(n):
@@ -142,15 +145,68 @@ def share_rccl_id(rank, world, make_id):
             time.sleep(0.2)
 
 
-def pmc_traffic(workload):
-    """HBM bytes per expand launch from a committed rocprofv3 PMC summary of
-    the same workload (profiles/pmc_<workload>.json, tools/pmc_summary.py)."""
+def pmc_summary(workload):
+    """The committed rocprofv3 summary of the same workload
+    (profiles/pmc_<workload>.json, tools/pmc_summary.py): HBM bytes per expand
+    launch from the PMC passes, and the rocprof expand time per timed search
+    of the traced bench command."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
     if not os.path.exists(path):
-        return None, None
+        return {}, None
     with open(path) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        return json.load(f), os.path.relpath(path, ROOT)
+
+
+def north_star(Engine, PAStarOpt, Sequences, device, searches=200, cpu_seconds=4.0):
+    """BASELINE.json's target config: PF08184 at 1 GPU, wall to the optimal
+    alignment (PairAlign + search + backtrace, one search per call) and
+    expansions/s, next to the CPU ports on the same host cores and the
+    reference's own -t 1 figure from the survey."""
+    name, (fasta_name, _, known) = "PF08184", WORKLOADS["PF08184"]
+    fasta = os.path.join(GOLDEN, fasta_name)
+    seqs = Sequences.from_fasta(fasta)
+    opt = PAStarOpt(profile=True)
+    t_cold = time.perf_counter()
+    eng = Engine(seqs, device=device)
+    t_ctx = time.perf_counter()
+    eng.init()
+    r = eng.pa_star(opt)
+    eng.alignment()
+    cold = time.perf_counter() - t_ctx
+    walls, exps, kern, loop = [], 0, 0.0, 0.0
+    for _ in range(searches):
+        t = time.perf_counter()
+        eng.init()
+        r = eng.pa_star(opt)
+        eng.alignment()
+        walls.append(time.perf_counter() - t)
+        if r.score != known:
+            raise RuntimeError("PF08184 score %d != %d" % (r.score, known))
+        exps += r.expansions_all
+        kern += r.expand_ms
+        loop += r.seconds
+    eng.close()
+    walls.sort()
+    wall = sum(walls) / len(walls)
+    rate = exps / sum(walls)
+    rec = {"workload": name, "baseline_config": WORKLOADS[name][1], "engine": "solo" if r.solo else "batched",
+           "searches": searches, "score": r.score, "score_ok": r.score == known,
+           "expansions_per_search": exps / searches, "wall_to_optimal_s": wall,
+           "wall_to_optimal_s_median": walls[len(walls) // 2], "nodes_per_s": rate,
+           "kernel_us_per_search": 1e3 * kern / searches, "launch_to_result_s": loop / searches,
+           "cold_context_wall_to_optimal_s": cold, "context_create_s": t_ctx - t_cold}
+    cpu = cpu_baseline(fasta, cpu_seconds, known)
+    rec["cpu_port"] = cpu["runs"]
+    for k, leg in cpu["runs"].items():
+        rec["ratio_nodes_per_s_vs_port_%s" % k] = rate / leg["value"]
+        rec["ratio_wall_vs_port_%s" % k] = leg["wall_to_optimal_s"] / wall
+    # the reference binary itself is unbuildable in this image (DESIGN.md
+    # §2); BASELINE.md §2 holds its -t 1 run from the survey container
+    rec["reference_t1_survey"] = {"wall_s": REF_PF08184_T1_S, "nodes_per_s": REF_PF08184_T1_NODES / REF_PF08184_T1_S,
+                                  "source": "BASELINE.md §2 (msa_pastar -t 1, survey container)"}
+    rec["ratio_nodes_per_s_vs_reference_t1"] = rate / (REF_PF08184_T1_NODES / REF_PF08184_T1_S)
+    rec["target"] = ">= 10x the CPU reference's nodes/s (BASELINE.json north_star)"
+    return rec
 
 
 def main():
@@ -168,6 +224,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-legs", default="t1,tN",
                     help="CPU baseline legs: t1 (serial), tN (multithreaded); syn8x400's serial search takes minutes")
+    ap.add_argument("--no-north-star", action="store_true", help="skip the PF08184 sub-record (N = 1 only)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "batched", "solo"], help="search engine")
     args = ap.parse_args()
 
     world = env_int("WORLD_SIZE", 1)
@@ -190,7 +248,7 @@ def main():
     device = env_int("PASTAR_BENCH_DEVICE", local_rank)  # override for single-GPU rehearsals
     engine = Engine(seqs, device=device, n_shards=world, shard_rank=rank, rccl_id=rid)
     opt = PAStarOpt(batch_nodes=args.batch, table_slots_log2=args.table_log2,
-                    pool_entries=args.pool, band=args.band, depth=args.depth, profile=True)
+                    pool_entries=args.pool, band=args.band, depth=args.depth, profile=True, mode=args.mode)
 
     def step():
         engine.init()
@@ -198,7 +256,14 @@ def main():
         rows = engine.alignment()
         return r, rows
 
-    for _ in range(args.warmup):
+    # the first search on this context: its buffers, the graph capture and
+    # the per-problem constants are set up inside it (untimed warmup)
+    engine.synchronize()
+    t_first = time.perf_counter()
+    step()
+    engine.synchronize()
+    first_search = time.perf_counter() - t_first
+    for _ in range(max(0, args.warmup - 1)):
         step()
 
     results = []
@@ -217,11 +282,14 @@ def main():
     select_ms = sum(r.select_ms for r, _ in results)
     gap_ms = sum(r.gap_ms for r, _ in results)
     launches = sum(r.expand_launches for r, _ in results)
-    wall = sum(r.seconds for r, _ in results) / len(results)
+    loop_s = sum(r.seconds for r, _ in results) / len(results)
     score = results[-1][0].score
     if dist_on:  # max over ranks (ns resolution)
-        mx = engine.allreduce([int(elapsed * 1e9), int(wall * 1e9)], "max")
-        elapsed, wall = mx[0] / 1e9, mx[1] / 1e9
+        mx = engine.allreduce([int(elapsed * 1e9), int(loop_s * 1e9), int(first_search * 1e9)], "max")
+        elapsed, loop_s, first_search = mx[0] / 1e9, mx[1] / 1e9, mx[2] / 1e9
+    # wall to the optimal alignment: a whole step (PairAlign, search,
+    # backtrace; inputs resident), as the metric names it
+    wall = elapsed / args.steps
         # the roofline is reported for rank 0's expand kernel
     if rank != 0:
         engine.barrier()
@@ -232,7 +300,30 @@ def main():
     b_exp = bytes_per_expansion(n)
     avg_launch_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = (exp_local / max(launches, 1)) * b_exp / avg_launch_s / 1e9 if launches else 0.0
-    traffic, traffic_src = pmc_traffic(args.workload)
+    pmc, traffic_src = pmc_summary(args.workload)
+    traffic = pmc.get("hbm_bytes_per_launch")
+    alg_per_launch = (exp_local / max(launches, 1)) * b_exp if launches else 0.0
+    exp_per_search = exp_local / args.steps
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "solo_kernel" if results[-1][0].solo else "expand_kernel", "bytes_per_expansion": b_exp,
+            "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
+            "avg_select_tail_us": 1e3 * select_ms / max(launches, 1),
+            "avg_gap_us": 1e3 * gap_ms / max(launches, 1),
+            "traffic_source": traffic_src}
+    if traffic and alg_per_launch:
+        # PMC bytes over algorithmic bytes per launch (> 1: re-reads and
+        # partial lines; the PMC read side is an upper bound, see the source)
+        roof["traffic_ratio"] = traffic / alg_per_launch
+    us_search = pmc.get("rocprof_expand_us_per_search_timed")
+    if us_search:
+        # the same algorithmic bytes per search over the expand time per
+        # search that rocprofv3 measured for this workload's bench command
+        # (profiles/, regenerated at the commit named there)
+        roof["frac_rocprof"] = exp_per_search * b_exp / (us_search * 1e-6) / 1e9 / HBM_PEAK_GBS
+        roof["rocprof_expand_us_per_search"] = us_search
+        roof["rocprof_commit"] = pmc.get("commit")
+        roof["rocprof_cmd"] = pmc.get("cmd")
     line = {
         "metric": METRIC,
         "value": value,
@@ -254,21 +345,21 @@ def main():
         "score": score,
         "score_ok": score == known,
         "wall_to_optimal_s": wall,
+        "search_loop_s": loop_s,
+        "first_search_on_context_s": first_search,
+        "first_over_warm": first_search / wall,
         "expansions_per_search": exp_all / args.steps,
         "steps_per_search": sum(r.steps for r, _ in results) / len(results),
+        "engine": "solo" if results[-1][0].solo else "batched",
         "graph_replay": bool(results[-1][0].graph_replay),
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "expand_kernel", "bytes_per_expansion": b_exp,
-                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
-                     "avg_select_tail_us": 1e3 * select_ms / max(launches, 1),
-                     "avg_gap_us": 1e3 * gap_ms / max(launches, 1),
-                     "traffic_source": traffic_src},
+        "roofline": roof,
     }
     if args.workload in SERIAL_EXPANSIONS:
         line["useful_rate"] = SERIAL_EXPANSIONS[args.workload] / wall
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fasta, args.cpu_seconds, known, tuple(args.cpu_legs.split(",")))
+    if world == 1 and not args.no_north_star and args.workload != "PF08184":
+        line["north_star"] = north_star(Engine, PAStarOpt, Sequences, device)
     print(json.dumps(line), flush=True)
     engine.barrier()
     engine.close()

@@ -41,14 +41,22 @@ def per_kernel(path, counter):
 
 
 def is_expand(name):
-    return "expand_kernel" in name and "expand_api" not in name
+    """The dominant search kernel: the batched engine's expand kernel, or the
+    LDS-resident search (one launch per search)."""
+    return ("expand_kernel" in name and "expand_api" not in name) or "solo_kernel" in name
+
+
+def is_search_start(name):
+    return "pairalign" in name or "solo_kernel" in name
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
     ap.add_argument("workload")
-    ap.add_argument("--round", default="r1")
+    ap.add_argument("--round", default="r2")
+    ap.add_argument("--commit", default="", help="commit the traced command ran at")
+    ap.add_argument("--cmd", default="", help="the traced bench command")
     args = ap.parse_args()
 
     stats_src = os.path.join(args.prof, "trace", "run_kernel_stats.csv")
@@ -69,12 +77,12 @@ def main():
         with open(bpath0) as f:
             lines0 = [l for l in f if l.startswith("{")]
         bench_pre = json.loads(lines0[-1]) if lines0 else None
-    timed_avg_us = timed_calls = None
+    timed_avg_us = timed_calls = per_search_us = None
     trace_path = os.path.join(args.prof, "trace", "run_kernel_trace.csv")
     if bench_pre and os.path.exists(trace_path):
         with open(trace_path) as f:
             rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
-        starts = [i for i, r in enumerate(rows) if "pairalign" in r["Kernel_Name"]]
+        starts = [i for i, r in enumerate(rows) if is_search_start(r["Kernel_Name"])]
         warm = bench_pre.get("warmup", 0)
         if len(starts) > warm:
             tail = rows[starts[warm]:]
@@ -82,6 +90,7 @@ def main():
             if d:
                 timed_avg_us = sum(d) / len(d) / 1e3
                 timed_calls = len(d)
+                per_search_us = sum(d) / bench_pre["steps"] / 1e3
 
     fetch = per_kernel(os.path.join(args.prof, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(args.prof, "write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -98,7 +107,7 @@ def main():
         bench = json.loads(lines[-1]) if lines else None
     out = {
         "workload": args.workload,
-        "kernel": "expand_kernel",
+        "kernel": "solo_kernel" if any("solo_kernel" in k for k in fetch) else "expand_kernel",
         "launches_fetch_pass": len(fk),
         "launches_write_pass": len(wk),
         "fetch_kib_per_launch_raw": fetch_kib,
@@ -111,6 +120,9 @@ def main():
         "rocprof_expand_calls": calls,
         "rocprof_avg_expand_us_timed_searches": timed_avg_us,
         "rocprof_expand_calls_timed_searches": timed_calls,
+        "rocprof_expand_us_per_search_timed": per_search_us,
+        "commit": args.commit,
+        "cmd": args.cmd,
         "kernel_stats": os.path.relpath(stats_dst, ROOT),
     }
     if bench:
