@@ -230,6 +230,52 @@ int pastar_gpu_closed_lookup(pastar_ctx *ctx, const uint16_t *pos, pastar_node *
  * receives the alignment length.  Collective over all shards. */
 int pastar_gpu_alignment(pastar_ctx *ctx, char *rows, int stride, int *cols);
 
+/* ---- OpenList / ClosedList (PriorityList<N>, PriorityList.h:52-122; the
+ * ClosedList map, PAStar.cpp:92; PAStar::enqueue, :219-237) ----
+ *
+ * The device search's own node table and f-bucket queues, driven one call at
+ * a time from the host: a loop shaped like worker_inner (PAStar.cpp:320-401)
+ * runs over these calls unchanged (include/pastar_lists.hpp wraps them as the
+ * reference's classes).  One node record serves both lists, so a node is in
+ * at most one of them; ties on g keep the smaller parent mask (the batched
+ * engine's rule) where the reference keeps the first found.  Single shard.
+ * A search (pastar_gpu_search) reuses the buffers and ends the session. */
+
+/* PAStar construction: empty lists (opts: table_slots_log2, pool_entries,
+ * subqueue_entries, band; zeros = defaults). */
+int pastar_gpu_lists_reset(pastar_ctx *ctx, const pastar_search_opts *opts);
+
+/* PAStar::enqueue + PriorityList::conditional_enqueue for each node: a node
+ * whose record (open or closed) has g <= node.g is discarded; else it
+ * (re)enters the OpenList with f = node.f.  added[i] (may be NULL) = 1 when
+ * node i entered; *reopened counts ClosedList nodes improved (nodes_reopen).
+ * PASTAR_ENOMEM (and the session ends) if a capacity ran out. */
+int pastar_gpu_open_enqueue(pastar_ctx *ctx, const pastar_node *nodes, int count, int32_t *added,
+                            int64_t *reopened);
+
+/* PriorityList::dequeue followed by the worker's ClosedList insert
+ * (worker_inner :336-351): up to max nodes, all with the lowest f of the
+ * OpenList (which of several ties is unspecified), move to the ClosedList
+ * and are written to out; *count = 0 when the OpenList is empty. */
+int pastar_gpu_open_dequeue(pastar_ctx *ctx, pastar_node *out, int max, int *count);
+
+/* PriorityList::get_highest_priority: the lowest f, INT32_MAX when empty. */
+int pastar_gpu_open_highest_priority(pastar_ctx *ctx, int32_t *f);
+
+/* PriorityList::size and the ClosedList map's size (nodes). */
+int pastar_gpu_lists_size(pastar_ctx *ctx, int64_t *open, int64_t *closed);
+
+/* OpenList.find / ClosedList.find: *where = 1 open, 2 closed, 0 absent; out
+ * (may be NULL) receives the node. */
+int pastar_gpu_lists_find(pastar_ctx *ctx, const uint16_t *pos, pastar_node *out, int *where);
+
+/* OpenList.erase (which = 1) / ClosedList.erase (which = 2): the node leaves
+ * the lists if it is in that one; *erased (may be NULL) = 1 if it was. */
+int pastar_gpu_lists_erase(pastar_ctx *ctx, const uint16_t *pos, int which, int *erased);
+
+/* Reopenings since pastar_gpu_lists_reset (nodes_reopen, PAStar.cpp:232). */
+int pastar_gpu_lists_reopened(pastar_ctx *ctx, int64_t *reopened);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,8 +6,8 @@ shards) runs as hand-written HIP kernels for gfx950 behind the C-ABI in
 include/pastar_gpu.h.  This package is the Python host mirror of the
 reference interface; see pastar.py.
 """
-from .pastar import (Engine, Node, PAStarOpt, SearchResult, Sequences, compute_weights, cost, get_id,
+from .pastar import (ClosedList, Engine, Node, PriorityList, PAStarOpt, SearchResult, Sequences, compute_weights, cost, get_id,
                      rccl_unique_id, sharded_search, similarity, ShardGroup)
 
-__all__ = ["Engine", "Node", "PAStarOpt", "SearchResult", "Sequences", "compute_weights", "cost", "get_id",
+__all__ = ["ClosedList", "Engine", "Node", "PriorityList", "PAStarOpt", "SearchResult", "Sequences", "compute_weights", "cost", "get_id",
            "rccl_unique_id", "sharded_search", "similarity", "ShardGroup"]

@@ -124,6 +124,20 @@ SIGNATURES = {
                                                 ctypes.POINTER(pastar_node)]),
     "pastar_gpu_alignment": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]),
+    # OpenList / ClosedList
+    "pastar_gpu_lists_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_search_opts)]),
+    "pastar_gpu_open_enqueue": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_node), ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_gpu_open_dequeue": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_node), ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int)]),
+    "pastar_gpu_open_highest_priority": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "pastar_gpu_lists_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_gpu_lists_find": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16),
+                                             ctypes.POINTER(pastar_node), ctypes.POINTER(ctypes.c_int)]),
+    "pastar_gpu_lists_erase": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16), ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_int)]),
+    "pastar_gpu_lists_reopened": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _lib = None

@@ -15,6 +15,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libpastar_gpu.so")
 CLI = os.path.join(HERE, "bin", "msa_pastar")
+LISTS_DEMO = os.path.join(HERE, "bin", "pastar_lists_astar")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off keeps the host weight pipeline in plain IEEE single
@@ -26,7 +27,7 @@ COMMON = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=
 COMMON += os.environ.get("PASTAR_HIPCC_FLAGS", "").split()
 
 LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp"]
-LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp"]
+LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp", "solo.hpp", "lists.hpp"]
 
 
 def _stale(target, deps):
@@ -69,9 +70,23 @@ def build_cli(force=False):
     return CLI
 
 
+def build_lists_demo(force=False):
+    """The reference's serial worker loop over the OpenList / ClosedList
+    facades (include/pastar_lists.hpp)."""
+    src = os.path.join(CSRC, "lists_astar_main.cpp")
+    deps = [src, LIB, os.path.join(ROOT, "include", "pastar_gpu.h"), os.path.join(ROOT, "include", "pastar_lists.hpp")]
+    if not force and not _stale(LISTS_DEMO, deps):
+        return LISTS_DEMO
+    os.makedirs(os.path.dirname(LISTS_DEMO), exist_ok=True)
+    _run(["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), src, "-o", LISTS_DEMO,
+          "-L" + HERE, "-lpastar_gpu", "-Wl,-rpath,$ORIGIN/.."])
+    return LISTS_DEMO
+
+
 def build_all(force=False):
     build_lib(force)
     build_cli(force)
+    build_lists_demo(force)
 
 
 if __name__ == "__main__":

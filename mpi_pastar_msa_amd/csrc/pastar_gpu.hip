@@ -32,6 +32,7 @@
 #include "host_model.hpp"
 #include "kernels.hpp"
 #include "pastar_gpu.h"
+#include "lists.hpp"
 #include "solo.hpp"
 
 using namespace pastar;
@@ -274,6 +275,13 @@ struct pastar_ctx {
     int solo_cap_log2 = 0;
     unsigned char *h_solo = nullptr;  // pinned copy of solo_buf
     size_t h_solo_n = 0;
+    // host-driven OpenList / ClosedList session (lists.hpp)
+    bool lists_ready = false;
+    SearchArgs lists_args{};
+    DevBuf<uint8_t> lists_io;           // nodes in / out, flags, results
+    unsigned char *h_lists = nullptr;   // pinned
+    size_t h_lists_n = 0;
+    long long lists_reopen = 0;
 
     // search state
     DevBuf<uint64_t> table;
@@ -675,6 +683,8 @@ void pastar_gpu_destroy(pastar_ctx *c)
         (void)hipHostFree(c->h_walk_masks);
     if (c->h_solo)
         (void)hipHostFree(c->h_solo);
+    if (c->h_lists)
+        (void)hipHostFree(c->h_lists);
     if (c->ev0)
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
@@ -1006,6 +1016,26 @@ int enqueue_walk(pastar_ctx *c, const uint16_t *pos, int total_len, bool local_o
     return PASTAR_OK;
 }
 
+// h of the origin and the automatic bucket width, once per context.
+int ensure_origin(pastar_ctx *c)
+{
+    if (c->origin_ready)
+        return PASTAR_OK;
+    uint16_t zero[PASTAR_MAX_SEQ] = {0};
+    DevBuf<uint16_t> dpos;
+    DevBuf<int32_t> dh;
+    PA_TRY(dpos.alloc(PASTAR_MAX_SEQ));
+    PA_TRY(dh.alloc(1));
+    HIP_TRY(hipMemcpy(dpos.p, zero, sizeof(zero), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(h_kernel, dim3(1), dim3(64), 0, c->stream, c->dP.p, dpos.p, 1, dh.p);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(&c->h0, dh.p, 4, hipMemcpyDeviceToHost));
+    PA_TRY(estimate_band_log2(c, c->h0, 0, &c->auto_band_log2));
+    c->origin_ready = true;
+    return PASTAR_OK;
+}
+
 template <int KWv>
 int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
 {
@@ -1021,19 +1051,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
 
     // h of the origin and the bucket width (once per context)
     uint16_t zero[PASTAR_MAX_SEQ] = {0};
-    if (!c->origin_ready) {
-        DevBuf<uint16_t> dpos;
-        DevBuf<int32_t> dh;
-        PA_TRY(dpos.alloc(PASTAR_MAX_SEQ));
-        PA_TRY(dh.alloc(1));
-        HIP_TRY(hipMemcpy(dpos.p, zero, sizeof(zero), hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(h_kernel, dim3(1), dim3(64), 0, c->stream, c->dP.p, dpos.p, 1, dh.p);
-        PA_TRY(check_launch());
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(hipMemcpy(&c->h0, dh.p, 4, hipMemcpyDeviceToHost));
-        PA_TRY(estimate_band_log2(c, c->h0, 0, &c->auto_band_log2));
-        c->origin_ready = true;
-    }
+    PA_TRY(ensure_origin(c));
     const int32_t h0 = c->h0;
     int w = c->auto_band_log2;
     if (cfg.band > 0)
@@ -1594,6 +1612,7 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     c->walk_ready = false;
     c->searched = false;
     c->score = -1;
+    c->lists_ready = false;  // the search reuses the list session's buffers
     if (!c->heuristic_ready)
         return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
     HIP_TRY(hipSetDevice(c->device));
@@ -1983,6 +2002,302 @@ int pastar_gpu_synchronize(pastar_ctx *c)
         return fail(PASTAR_EINVAL, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipDeviceSynchronize());
+    return PASTAR_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// OpenList / ClosedList (lists.hpp): host-driven operations on the device
+// node table and f-bucket queues.
+// ===========================================================================
+namespace {
+
+int lists_check(pastar_ctx *c)
+{
+    if (!c)
+        return fail(PASTAR_EINVAL, "null ctx");
+    if (!c->lists_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_lists_reset not called (or a search ran since)");
+    HIP_TRY(hipSetDevice(c->device));
+    return PASTAR_OK;
+}
+
+// device scratch (lists_io) and its pinned mirror (h_lists), grown on demand
+int lists_io(pastar_ctx *c, size_t bytes)
+{
+    if (c->lists_io.n < bytes)
+        PA_TRY(c->lists_io.alloc(std::max<size_t>(bytes, 4096)));
+    if (c->h_lists_n < bytes) {
+        if (c->h_lists)
+            (void)hipHostFree(c->h_lists);
+        c->h_lists = nullptr;
+        c->h_lists_n = 0;
+        const size_t n = std::max<size_t>(bytes, 4096);
+        HIP_TRY(hipHostMalloc((void **)&c->h_lists, n, hipHostMallocDefault));
+        c->h_lists_n = n;
+    }
+    return PASTAR_OK;
+}
+
+int check_coord(const pastar_ctx *c, const uint16_t *pos)
+{
+    for (int i = 0; i < c->n; i++)
+        if (pos[i] > c->hp.len[i])
+            return fail(PASTAR_EINVAL, "coordinate outside the lattice");
+    return PASTAR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
+{
+    if (!c)
+        return fail(PASTAR_EINVAL, "null ctx");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    if (c->tr)
+        return fail(PASTAR_EINVAL, "the host-driven lists are single-shard");
+    HIP_TRY(hipSetDevice(c->device));
+    pastar_search_opts o{};
+    if (opts)
+        o = *opts;
+    c->lists_ready = false;
+    c->searched = false;
+    c->walk_ready = false;
+    c->solo_active = false;
+    PA_TRY(ensure_hc(c));
+    PA_TRY(ensure_origin(c));
+    SearchCfg cfg{};
+    cfg.kmax = cfg.kmin = 1;
+    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 20;
+    if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
+        return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
+    cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 22);
+    cfg.subqueue_entries = o.subqueue_entries > 0 ? (unsigned long long)o.subqueue_entries : (1ull << 18);
+    cfg.outbox_cap = 1;
+    PA_TRY(alloc_search(c, cfg));
+    int w = c->auto_band_log2;
+    if (o.band > 0)
+        PA_TRY(estimate_band_log2(c, c->h0, o.band, &w));
+    Ctl hc{};
+    hc.band_log2 = w;
+    hc.f0 = c->h0;
+    hc.n_shards = 1;
+    hc.kmax = hc.kmin = 1;
+    hc.pool_chunks = pool_chunks_of(cfg);
+    hc.maxch = maxch_of(cfg);
+    hc.table_slots = c->nslots;
+    hc.cur_b = kBuckets;  // empty: appends lower it
+    std::memcpy(c->h_stage, &hc, sizeof(Ctl));
+    HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    SearchArgs &a = c->lists_args;
+    a = SearchArgs{};
+    a.P = c->dP.p;
+    a.ctl = c->ctl.p;
+    a.stamps = c->stamps.p;
+    a.table = c->table.p;
+    a.cap_mask = c->nslots - 1;
+    a.q = c->queues.p;
+    a.chunk_tab = c->chunk_tab.p;
+    a.pool = c->pool.p;
+    a.stats = c->stats.p;
+    a.goal_g = c->goal.p;
+    a.maxch = maxch_of(cfg);
+    a.pool_chunks = pool_chunks_of(cfg);
+    c->lists_reopen = 0;
+    c->lists_ready = true;
+    return PASTAR_OK;
+}
+
+int pastar_gpu_open_enqueue(pastar_ctx *c, const pastar_node *nodes, int count, int32_t *added, int64_t *reopened)
+{
+    PA_TRY(lists_check(c));
+    if (count < 0 || (!nodes && count))
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    if (reopened)
+        *reopened = 0;
+    if (count == 0)
+        return PASTAR_OK;
+    for (int k = 0; k < count; k++) {
+        PA_TRY(check_coord(c, nodes[k].pos));
+        if (nodes[k].g < 0 || nodes[k].f < nodes[k].g)
+            return fail(PASTAR_EINVAL, "node %d: g %d, f %d", k, nodes[k].g, nodes[k].f);
+    }
+    const size_t nb = sizeof(pastar_node) * (size_t)count, fb = 4 * (size_t)count;
+    const size_t off_flags = (nb + 15) & ~(size_t)15, off_res = (off_flags + fb + 15) & ~(size_t)15;
+    PA_TRY(lists_io(c, off_res + 64));
+    uint8_t *d = c->lists_io.p;
+    std::memcpy(c->h_lists, nodes, nb);
+    HIP_TRY(hipMemcpyAsync(d, c->h_lists, nb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d + off_res, 0, 16, c->stream));
+    HIP_TRY(hipMemsetAsync(&c->stats.p->ovf_near, 0, 16, c->stream));
+    const dim3 grid((unsigned)((count + kListThreads - 1) / kListThreads));
+    const pastar_node *din = reinterpret_cast<const pastar_node *>(d);
+    int32_t *dflags = reinterpret_cast<int32_t *>(d + off_flags);
+    unsigned long long *dres = reinterpret_cast<unsigned long long *>(d + off_res);
+    if (c->kw == 1)
+        hipLaunchKernelGGL(lists_enqueue_kernel<1>, grid, dim3(kListThreads), 0, c->stream, c->lists_args, din, count,
+                           dflags, dres);
+    else if (c->kw == 2)
+        hipLaunchKernelGGL(lists_enqueue_kernel<2>, grid, dim3(kListThreads), 0, c->stream, c->lists_args, din, count,
+                           dflags, dres);
+    else
+        hipLaunchKernelGGL(lists_enqueue_kernel<4>, grid, dim3(kListThreads), 0, c->stream, c->lists_args, din, count,
+                           dflags, dres);
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemcpyAsync(c->h_lists + off_flags, dflags, fb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_lists + off_res, dres, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 16, &c->stats.p->ovf_near, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned long long *r = reinterpret_cast<const unsigned long long *>(c->h_lists + off_res);
+    if (r[1] || r[2] || r[3]) {
+        c->lists_ready = false;  // a node was dropped: the lists are no longer exact
+        return fail(PASTAR_ENOMEM, "OpenList capacity exhausted (table %llu, pool %llu, sub-queue %llu drops); "
+                    "reset with larger capacities", r[1], r[2], r[3]);
+    }
+    if (added)
+        std::memcpy(added, c->h_lists + off_flags, fb);
+    c->lists_reopen += (long long)r[0];
+    if (reopened)
+        *reopened = (int64_t)r[0];
+    return PASTAR_OK;
+}
+
+static int lists_pop(pastar_ctx *c, pastar_node *out, int max, int peek, int res[3])
+{
+    PA_TRY(lists_io(c, 64 + sizeof(pastar_node) * (size_t)std::max(max, 1)));
+    uint8_t *d = c->lists_io.p;
+    int *dres = reinterpret_cast<int *>(d);
+    pastar_node *dout = reinterpret_cast<pastar_node *>(d + 64);
+    if (c->kw == 1)
+        hipLaunchKernelGGL(lists_dequeue_kernel<1>, dim3(1), dim3(kListThreads), 0, c->stream, c->lists_args, dout, max,
+                           peek, dres);
+    else if (c->kw == 2)
+        hipLaunchKernelGGL(lists_dequeue_kernel<2>, dim3(1), dim3(kListThreads), 0, c->stream, c->lists_args, dout, max,
+                           peek, dres);
+    else
+        hipLaunchKernelGGL(lists_dequeue_kernel<4>, dim3(1), dim3(kListThreads), 0, c->stream, c->lists_args, dout, max,
+                           peek, dres);
+    PA_TRY(check_launch());
+    const size_t ob = peek ? 0 : sizeof(pastar_node) * (size_t)max;
+    HIP_TRY(hipMemcpyAsync(c->h_lists, d, 64 + ob, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memcpy(res, c->h_lists, 12);
+    if (!peek && res[0] > 0)
+        std::memcpy(out, c->h_lists + 64, sizeof(pastar_node) * (size_t)res[0]);
+    return PASTAR_OK;
+}
+
+int pastar_gpu_open_dequeue(pastar_ctx *c, pastar_node *out, int max, int *count)
+{
+    PA_TRY(lists_check(c));
+    if (!out || !count || max < 1)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    int res[3];
+    PA_TRY(lists_pop(c, out, max, 0, res));
+    *count = res[0];
+    c->lists_reopen += res[2];
+    return PASTAR_OK;
+}
+
+int pastar_gpu_open_highest_priority(pastar_ctx *c, int32_t *f)
+{
+    PA_TRY(lists_check(c));
+    if (!f)
+        return fail(PASTAR_EINVAL, "null argument");
+    int res[3];
+    PA_TRY(lists_pop(c, nullptr, 1, 1, res));
+    *f = res[1];
+    return PASTAR_OK;
+}
+
+int pastar_gpu_lists_size(pastar_ctx *c, int64_t *open, int64_t *closed)
+{
+    PA_TRY(lists_check(c));
+    PA_TRY(lists_io(c, 64));
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(c->lists_io.p);
+    HIP_TRY(hipMemsetAsync(d, 0, 16, c->stream));
+    const unsigned blocks = (unsigned)std::min<uint64_t>(1024, (c->nslots + kListThreads - 1) / kListThreads);
+    if (c->kw == 1)
+        hipLaunchKernelGGL(lists_census_kernel<1>, dim3(blocks), dim3(kListThreads), 0, c->stream, c->table.p, c->nslots, d);
+    else if (c->kw == 2)
+        hipLaunchKernelGGL(lists_census_kernel<2>, dim3(blocks), dim3(kListThreads), 0, c->stream, c->table.p, c->nslots, d);
+    else
+        hipLaunchKernelGGL(lists_census_kernel<4>, dim3(blocks), dim3(kListThreads), 0, c->stream, c->table.p, c->nslots, d);
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemcpyAsync(c->h_lists, d, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const unsigned long long *h = reinterpret_cast<const unsigned long long *>(c->h_lists);
+    if (open)
+        *open = (int64_t)h[0];
+    if (closed)
+        *closed = (int64_t)h[1];
+    return PASTAR_OK;
+}
+
+static int lists_find_erase(pastar_ctx *c, const uint16_t *pos, int erase_which, unsigned long long r[3])
+{
+    PA_TRY(lists_io(c, 128));
+    uint8_t *d = c->lists_io.p;
+    std::memcpy(c->h_lists + 64, pos, 2 * PASTAR_MAX_SEQ);
+    HIP_TRY(hipMemcpyAsync(d + 64, c->h_lists + 64, 2 * PASTAR_MAX_SEQ, hipMemcpyHostToDevice, c->stream));
+    const uint16_t *dpos = reinterpret_cast<const uint16_t *>(d + 64);
+    unsigned long long *dres = reinterpret_cast<unsigned long long *>(d);
+    if (c->kw == 1)
+        hipLaunchKernelGGL(lists_find_kernel<1>, dim3(1), dim3(1), 0, c->stream, c->lists_args, dpos, erase_which, dres);
+    else if (c->kw == 2)
+        hipLaunchKernelGGL(lists_find_kernel<2>, dim3(1), dim3(1), 0, c->stream, c->lists_args, dpos, erase_which, dres);
+    else
+        hipLaunchKernelGGL(lists_find_kernel<4>, dim3(1), dim3(1), 0, c->stream, c->lists_args, dpos, erase_which, dres);
+    PA_TRY(check_launch());
+    HIP_TRY(hipMemcpyAsync(c->h_lists, d, 24, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memcpy(r, c->h_lists, 24);
+    return PASTAR_OK;
+}
+
+int pastar_gpu_lists_find(pastar_ctx *c, const uint16_t *pos, pastar_node *out, int *where)
+{
+    PA_TRY(lists_check(c));
+    if (!pos || !where)
+        return fail(PASTAR_EINVAL, "null argument");
+    PA_TRY(check_coord(c, pos));
+    unsigned long long r[3];
+    PA_TRY(lists_find_erase(c, pos, 0, r));
+    *where = (int)r[0];
+    if (out && r[0]) {
+        std::memset(out, 0, sizeof(*out));
+        std::memcpy(out->pos, pos, sizeof(uint16_t) * c->n);
+        out->g = (int32_t)(r[1] >> 32);
+        out->parent_mask = (int32_t)(uint32_t)r[1];
+        out->f = out->g + (int32_t)(r[2] >> 32);
+    }
+    return PASTAR_OK;
+}
+
+int pastar_gpu_lists_erase(pastar_ctx *c, const uint16_t *pos, int which, int *erased)
+{
+    PA_TRY(lists_check(c));
+    if (!pos || (which != 1 && which != 2))
+        return fail(PASTAR_EINVAL, "invalid arguments (which: 1 OpenList, 2 ClosedList)");
+    PA_TRY(check_coord(c, pos));
+    unsigned long long r[3];
+    PA_TRY(lists_find_erase(c, pos, which, r));
+    if (erased)
+        *erased = (int)r[0] == which ? 1 : 0;
+    return PASTAR_OK;
+}
+
+int pastar_gpu_lists_reopened(pastar_ctx *c, int64_t *reopened)
+{
+    PA_TRY(lists_check(c));
+    if (!reopened)
+        return fail(PASTAR_EINVAL, "null argument");
+    *reopened = c->lists_reopen;
     return PASTAR_OK;
 }
 

@@ -361,6 +361,121 @@ class Engine:
         return [raw[i * stride:i * stride + cols.value].decode("latin-1") for i in range(self.n)]
 
 
+def _c_nodes(nodes):
+    arr = (nat.pastar_node * max(len(nodes), 1))()
+    for k, nd in enumerate(nodes):
+        for i, c in enumerate(nd.pos):
+            arr[k].pos[i] = c
+        arr[k].g, arr[k].f, arr[k].parent_mask = nd.g, nd.f, nd.parenti
+    return arr
+
+
+def _c_coord(coord):
+    c = (ctypes.c_uint16 * nat.MAX_SEQ)()
+    for i, v in enumerate(coord):
+        c[i] = v
+    return c
+
+
+class PriorityList:
+    """The OpenList (PriorityList<N>, PriorityList.h:52-122) on the device:
+    the engine's node table and f-bucket queues driven one call at a time
+    (pastar_gpu_lists_reset / open_* in include/pastar_gpu.h).  Construct it
+    to start an empty OpenList + ClosedList pair on the engine's context."""
+
+    def __init__(self, engine, opt=None):
+        self.engine = engine
+        so = (opt or PAStarOpt()).search_opts()
+        check(lib().pastar_gpu_lists_reset(engine._ctx, ctypes.byref(so)))
+        self.closed = ClosedList(engine)
+
+    def dequeue(self):
+        """PriorityList::dequeue + the worker's ClosedList insert: a node of
+        the lowest f, or None when the OpenList is empty."""
+        got = self.dequeue_batch(1)
+        return got[0] if got else None
+
+    def dequeue_batch(self, max_nodes):
+        """Up to max_nodes nodes, all of the lowest f."""
+        out = (nat.pastar_node * max_nodes)()
+        cnt = ctypes.c_int()
+        check(lib().pastar_gpu_open_dequeue(self.engine._ctx, out, max_nodes, ctypes.byref(cnt)))
+        n = self.engine.n
+        return [Node(tuple(out[k].pos[:n]), out[k].g, out[k].f, out[k].parent_mask) for k in range(cnt.value)]
+
+    def conditional_enqueue(self, nodes):
+        """PAStar::enqueue over a batch (the ClosedList check, then
+        PriorityList::conditional_enqueue): which nodes entered the OpenList."""
+        nodes = list(nodes) if not isinstance(nodes, Node) else [nodes]
+        if not nodes:
+            return []
+        added = (ctypes.c_int32 * len(nodes))()
+        reop = ctypes.c_int64()
+        check(lib().pastar_gpu_open_enqueue(self.engine._ctx, _c_nodes(nodes), len(nodes), added,
+                                            ctypes.byref(reop)))
+        return [bool(a) for a in added]
+
+    enqueue = conditional_enqueue
+
+    def get_highest_priority(self):
+        f = ctypes.c_int32()
+        check(lib().pastar_gpu_open_highest_priority(self.engine._ctx, ctypes.byref(f)))
+        return f.value
+
+    def size(self):
+        o, c = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().pastar_gpu_lists_size(self.engine._ctx, ctypes.byref(o), ctypes.byref(c)))
+        return o.value
+
+    def empty(self):
+        return self.get_highest_priority() == 2 ** 31 - 1
+
+    def find(self, coord):
+        """The OpenList's node at coord, or None."""
+        nd, where = self.closed._find(coord)
+        return nd if where == 1 else None
+
+    def erase(self, coord):
+        e = ctypes.c_int()
+        check(lib().pastar_gpu_lists_erase(self.engine._ctx, _c_coord(coord), 1, ctypes.byref(e)))
+        return e.value
+
+    def reopened(self):
+        r = ctypes.c_int64()
+        check(lib().pastar_gpu_lists_reopened(self.engine._ctx, ctypes.byref(r)))
+        return r.value
+
+
+class ClosedList:
+    """The ClosedList (std::map<Coord<N>, Node<N>>, PAStar.cpp:92) of the same
+    device session: nodes enter it through PriorityList.dequeue."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def _find(self, coord):
+        out = nat.pastar_node()
+        where = ctypes.c_int()
+        check(lib().pastar_gpu_lists_find(self.engine._ctx, _c_coord(coord), ctypes.byref(out), ctypes.byref(where)))
+        if not where.value:
+            return None, 0
+        return Node(tuple(out.pos[:self.engine.n]), out.g, out.f, out.parent_mask), where.value
+
+    def find(self, coord):
+        nd, where = self._find(coord)
+        return nd if where == 2 else None
+
+    def erase(self, coord):
+        e = ctypes.c_int()
+        check(lib().pastar_gpu_lists_erase(self.engine._ctx, _c_coord(coord), 2, ctypes.byref(e)))
+        return e.value
+
+    def size(self):
+        o, c = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().pastar_gpu_lists_size(self.engine._ctx, ctypes.byref(o), ctypes.byref(c)))
+        return c.value
+
+
 def sharded_search(sequences, n_shards, devices=(0,), opt=None, **engine_kw):
     """One search sharded over `n_shards` contexts of this process (one host
     thread each, ShardGroup transport); devices are used round-robin.
