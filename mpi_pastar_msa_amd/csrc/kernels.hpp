@@ -90,7 +90,11 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int x = P.pair_x[p], y = P.pair_y[p], wgt = P.weight[p];
     const int L1 = P.len[x], L2 = P.len[y];
-    const int GO = P.gap_open, GE = P.gap_ext;
+    // the search form alone with equal gap costs: the sweep runs in weighted
+    // units (w * H: min and + commute with w >= 0, so every cell equals H * w)
+    // on a distance table staged pre-weighted, with no multiply in the loop
+    constexpr bool WEIGHTED = EQ_GAPS && !WRITE_H && SUB_LDS;
+    const int GO = WEIGHTED ? P.gap_open * wgt : P.gap_open, GE = P.gap_ext;
     const int alpha = P.alpha;
     const uint8_t *s1 = P.codes + P.seq_off[x];
     const uint8_t *s2g = P.codes + P.seq_off[y];
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
         s2[k] = s2g[k];
     if (SUB_LDS)
         for (int k = threadIdx.x; k < alpha * alpha; k += blockDim.x)
-            sub[k] = P.sub[k];
+            sub[k] = WEIGHTED ? P.sub[k] * wgt : P.sub[k];
     if (threadIdx.x < kPaWaves)
         progress[threadIdx.x] = -1;
     const int32_t *subp;
@@ -157,14 +161,28 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
             // band's top row (lane 63) and the distance row for columns
             // j0 - 1 .. j0 - 8 (the cost of step u + 1)
             int lb[kPaChunk], lbd[kPaChunk], nc[kPaChunk];
+            if constexpr (EQ_GAPS) {
+                // unclamped: a column outside the table only feeds cells
+                // outside the table (a lane's column is its neighbour's of
+                // the step before, minus one), so what those reads return
+                // is never used; lb is lane 63's row below (+inf under the
+                // table), the old value of the DPP shift below
 #pragma unroll
-            for (int u = 0; u < kPaChunk; u++) {
-                const int jj = j0 - u;
-                const int jc = jj < 0 ? 0 : (jj > L2 ? L2 : jj);
-                const int jn = jj - 1 < 0 ? 0 : (jj - 1 > L2 ? L2 : jj - 1);
-                lb[u] = below[jc];
-                lbd[u] = EQ_GAPS ? 0 : belowd[jc];
-                nc[u] = s2[jn];
+                for (int u = 0; u < kPaChunk; u++) {
+                    lb[u] = band > 0 ? below[j0 - u] : kPaInf;
+                    lbd[u] = 0;
+                    nc[u] = s2[j0 - u - 1];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kPaChunk; u++) {
+                    const int jj = j0 - u;
+                    const int jc = jj < 0 ? 0 : (jj > L2 ? L2 : jj);
+                    const int jn = jj - 1 < 0 ? 0 : (jj - 1 > L2 ? L2 : jj - 1);
+                    lb[u] = below[jc];
+                    lbd[u] = belowd[jc];
+                    nc[u] = s2[jn];
+                }
             }
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++)
@@ -183,9 +201,10 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 const int cost_here = cost;
                 cost = nc[u];
                 if constexpr (EQ_GAPS) {
-                    const int m_up = from_lane_above_inf(m);
+                    // lane 63 has no lane above: the shift leaves it the old
+                    // value, the previous band's top row (or +inf)
                     diag = down;
-                    down = use_lds_below ? lb[u] : m_up;
+                    down = __builtin_amdgcn_update_dpp(lb[u], m, 0x130, 0xf, 0xf, false);
                     const int right = m;
                     mm = (down < right ? down : right) + GO;
                     const int c2 = diag + cost_here;
@@ -212,8 +231,13 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                     aa = last_row ? (last_col ? kNoGap : kGapY) : (last_col ? kGapX : aa);
                 }
                 // unsigned: cells outside the table may hold +inf, never stored
-                cb[u] = make_int2((int)((unsigned)mm * (unsigned)wgt), cost_here * wgt);
-                m = in ? mm : m;
+                if constexpr (WEIGHTED)
+                    cb[u] = make_int2(mm, cost_here);
+                else
+                    cb[u] = make_int2((int)((unsigned)mm * (unsigned)wgt), cost_here * wgt);
+                // a column left of the table only feeds cells left of it:
+                // only the columns right of it must stay +inf
+                m = (EQ_GAPS ? j <= L2 : in) ? mm : m;
                 a = EQ_GAPS ? 0 : (in ? aa : a);
                 tb[u] = m;
                 tbd[u] = a;

@@ -1465,6 +1465,8 @@ bool solo_plan(const pastar_ctx *c, SoloPlan *pl)
     off = align16(off + (size_t)c->hp.alpha * c->hp.alpha * 4);
     a.off_codes = (int)off;
     off = align16(off + c->codes_len);
+    a.off_subw = (int)off;  // a pre-weighted distance table per wave
+    off = align16(off + (size_t)(kSoloThreads / 64) * (c->hp.alpha * c->hp.alpha + 1) * 4);
     if (off >= (size_t)kSoloLds)
         return false;
     int lg = kSoloMaxCapLog2;

@@ -65,7 +65,7 @@ struct SoloArgs {
     const int32_t *sub;
     long long max_levels;
     int cap_log2, max_path, hc_cells, codes_len, alpha2;
-    int off_prob, off_sub, off_codes, off_keys, off_best, off_hcl, off_open, off_batch;  // LDS bytes
+    int off_prob, off_sub, off_codes, off_keys, off_best, off_hcl, off_open, off_batch, off_subw;  // LDS bytes
     int band_log2;  // < 0: the engine's automatic band (pastar_gpu.hip estimate_band_log2)
 };
 
@@ -117,12 +117,18 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // in weighted units.  Bands of 64 rows run one after the other on the same
 // wave; lane 63 of band k reads the row below from band k - 1's top row in T.
 __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int p, SOLO_LDS solo_v2 *HCl,
-                                               const SOLO_LDS int *sub, const SOLO_LDS uint8_t *codes)
+                                               const SOLO_LDS int *sub, const SOLO_LDS uint8_t *codes,
+                                               SOLO_LDS int *subw)
 {
     const int lane = lane_id();
     const int x = P.pair_x[p], y = P.pair_y[p], wgt = P.weight[p];
     const int L1 = P.len[x], L2 = P.len[y], W = L2 + 1, alpha = P.alpha;
     const int GO = P.gap_open * wgt;
+    // the wave's copy of the distance table, pre-weighted: no multiply in
+    // the sweep
+    for (int k = lane; k < alpha * alpha; k += 64)
+        subw[k] = sub[k] * wgt;
+    lds_fence();
     const SOLO_LDS uint8_t *s1 = codes + P.seq_off[x];
     const SOLO_LDS uint8_t *s2 = codes + P.seq_off[y];
     SOLO_LDS solo_v2 *T = HCl + P.h_off[p];
@@ -132,9 +138,8 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
         const int i = bottom - (63 - lane);
         const bool row_ok = i >= 0;
         const int cx = row_ok ? (int)s1[i] : 0;  // code 0 at i == L1 (string end)
-        const SOLO_LDS int *crow = sub + cx * alpha;
+        const SOLO_LDS int *crow = subw + cx * alpha;
         const bool last_row = i == L1;
-        const bool use_below = lane == 63 && band > 0;
         const SOLO_LDS solo_v2 *below = T + (bottom + 1) * W;  // band - 1's top row (band > 0)
         SOLO_LDS solo_v2 *Trow = T + (row_ok ? i : 0) * W;
         int m = kPaInf, down = kPaInf, diag = 0;
@@ -146,14 +151,14 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
         const int nsteps = L2 + 1 + (bottom < 63 ? bottom : 63);
         for (int t0 = 0; t0 < nsteps; t0 += kPaChunk) {
             const int j0 = j;
+            // unclamped (as in pairalign_wave_kernel): a column outside the
+            // table only feeds cells outside it; lb is lane 63's row below
+            // (+inf under the table), the old value of the DPP shift
             int lb[kPaChunk], nc[kPaChunk];
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++) {
-                const int jj = j0 - u;
-                const int jc = jj < 0 ? 0 : (jj > L2 ? L2 : jj);
-                const int jn = jj - 1 < 0 ? 0 : (jj - 1 > L2 ? L2 : jj - 1);
-                lb[u] = use_below ? below[jc].x : 0;
-                nc[u] = s2[jn];
+                lb[u] = band > 0 ? below[j0 - u].x : kPaInf;
+                nc[u] = s2[j0 - u - 1];
             }
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++)
@@ -161,18 +166,16 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
             solo_v2 cb[kPaChunk];
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++, j--) {
-                const bool in = row_ok && j >= 0 && j <= L2;
-                const int cost_here = cost * wgt;
+                const int cost_here = cost;
                 cost = nc[u];
-                const int m_up = from_lane_above_inf(m);
                 diag = down;
-                down = use_below ? lb[u] : m_up;
+                down = __builtin_amdgcn_update_dpp(lb[u], m, 0x130, 0xf, 0xf, false);
                 int mm = (down < m ? down : m) + GO;
                 const int c2 = diag + cost_here;
                 mm = c2 < mm ? c2 : mm;
                 mm = (last_row && t0 + u == 0) ? 0 : mm;  // the corner (L1, L2)
                 cb[u] = solo_v2{mm, cost_here};
-                m = in ? mm : m;
+                m = j <= L2 ? mm : m;  // only the columns right of the table stay +inf
             }
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++) {
@@ -306,8 +309,9 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     const SOLO_LDS DevProblem &P = *Pl;
 
     // 1. PairAlign, pair p on wave p % 4
+    SOLO_LDS int *subw = lds_at<int>(smem, a.off_subw) + wave * (a.alpha2 + 1);
     for (int p = wave; p < NP; p += kSoloThreads / 64)
-        solo_pairalign(P, p, HCl, sub, codes);
+        solo_pairalign(P, p, HCl, sub, codes, subw);
     __syncthreads();
     if (wave != 0)
         return;
