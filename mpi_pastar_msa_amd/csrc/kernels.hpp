@@ -1586,8 +1586,14 @@ __global__ void queue_reset_kernel(Queues *__restrict__ q, uint32_t *__restrict_
 
 // Open entries left in the queues (current or superseded), for the
 // statistics: one read of every cursor pair.
-__global__ void queue_census_kernel(const Queues *__restrict__ q, unsigned long long *__restrict__ out)
+// gate (may be null): run only when the search ended with the goal found
+// (*gate == 1, Ctl::status), so the host may enqueue it behind a graph
+// replay before knowing whether that replay finished the search
+__global__ void queue_census_kernel(const Queues *__restrict__ q, unsigned long long *__restrict__ out,
+                                    const int *__restrict__ gate)
 {
+    if (gate && *(volatile const int *)gate != 1)
+        return;
     unsigned long long s = 0;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < kBuckets * kSub; k += gridDim.x * blockDim.x)
         s += q->W[k / kSub][k % kSub] - q->R[k / kSub][k % kSub];
@@ -1643,8 +1649,11 @@ __global__ __launch_bounds__(kBlock) void open_census_kernel(SearchArgs a, int g
 template <int N, int KW>
 __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table, uint64_t cap_mask,
                             const uint64_t *__restrict__ start, int max, int local_only,
-                            int32_t *__restrict__ masks, uint64_t *__restrict__ last_key, int *__restrict__ info)
+                            int32_t *__restrict__ masks, uint64_t *__restrict__ last_key, int *__restrict__ info,
+                            const int *__restrict__ gate)
 {
+    if (gate && *(volatile const int *)gate != 1)  // see queue_census_kernel
+        return;
     const DevProblem &Pg = *Pp;
     const int n = N ? N : Pg.n;
     constexpr int SW = slot_words<KW>();

@@ -494,7 +494,7 @@ struct Ops {
     void (*expand)(dim3, dim3, hipStream_t, const SearchArgs &);
     void (*insert_remote)(dim3, dim3, hipStream_t, const SearchArgs &, const void *, unsigned long long);
     void (*walk)(hipStream_t, const DevProblem *, const uint64_t *, uint64_t, const uint64_t *, int, int, int32_t *,
-                 uint64_t *, int *);
+                 uint64_t *, int *, const int *);
     void (*lookup)(hipStream_t, const uint64_t *, uint64_t, const uint64_t *, uint64_t *);
 };
 
@@ -515,9 +515,10 @@ struct Impl {
         hipLaunchKernelGGL((insert_remote_kernel<KW>), g, b, 0, s, a, (const Remote<KW> *)recs, count);
     }
     static void walk(hipStream_t s, const DevProblem *P, const uint64_t *t, uint64_t cm, const uint64_t *start, int max,
-                     int local, int32_t *masks, uint64_t *last, int *info)
+                     int local, int32_t *masks, uint64_t *last, int *info, const int *gate)
     {
-        hipLaunchKernelGGL((walk_kernel<N, KW>), dim3(1), dim3(1), 0, s, P, t, cm, start, max, local, masks, last, info);
+        hipLaunchKernelGGL((walk_kernel<N, KW>), dim3(1), dim3(1), 0, s, P, t, cm, start, max, local, masks, last, info,
+                           gate);
     }
     static void lookup(hipStream_t s, const uint64_t *t, uint64_t cm, const uint64_t *key, uint64_t *out)
     {
@@ -1011,7 +1012,7 @@ int enqueue_walk(pastar_ctx *c, const uint16_t *pos, int total_len, bool local_o
     if (c->solo_active)  // a solo search walks its own chain (solo.hpp)
         return fail(PASTAR_ESTATE, "no node table walk after an LDS-resident search");
     ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_key.p, total_len + 1, local_only ? 1 : 0,
-             c->walk_masks.p, c->walk_last.p, c->walk_info.p);
+             c->walk_masks.p, c->walk_last.p, c->walk_info.p, nullptr);
     PA_TRY(check_launch());
     return PASTAR_OK;
 }
@@ -1224,6 +1225,45 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         }
         long long steps_before = 0;
         int rc = PASTAR_OK;
+        // the end-of-search work rides behind every replay, gated on the
+        // device-side status (queue_census_kernel, walk_kernel): the replay
+        // that finishes the search is followed by the census of the open
+        // list and the backtrace walk from the goal in the same stream, and
+        // the one host round trip returns all of it
+        int total_len = 0;
+        uint16_t goal_pos[PASTAR_MAX_SEQ] = {0};
+        for (int i = 0; i < c->n; i++) {
+            total_len += c->hp.len[i];
+            goal_pos[i] = (uint16_t)c->hp.len[i];
+        }
+        PA_TRY(ensure_walk_buffers(c, total_len));
+        if (!c->census.p)
+            PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
+        HIP_TRY(hipMemsetAsync(c->census.p, 0, 24, c->stream));
+        HIP_TRY(hipMemsetAsync(c->census.p + 3, 0xff, 16, c->stream));
+        pack_key(c, goal_pos, c->h_walk);
+        HIP_TRY(hipMemcpyAsync(c->walk_key.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+        unsigned long long *cz_tail = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
+        int32_t *goal_tail = reinterpret_cast<int32_t *>(c->h_stage + 128);
+        const int *gate = &c->ctl.p->status;
+        auto enqueue_tail = [&]() -> hipError_t {
+            hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, c->census.p, gate);
+            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_key.p, total_len + 1, 0, c->walk_masks.p,
+                     c->walk_last.p, c->walk_info.p, gate);
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(goal_tail, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(cz_tail, c->census.p, 40, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->h_walk + 4, c->walk_info.p, 8, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->h_walk_masks, c->walk_masks.p, 4 * ((size_t)total_len + 1),
+                                   hipMemcpyDeviceToHost, c->stream);
+            return e;
+        };
         for (;;) {
             // long runs until the predicted end is near, then short ones: a
             // launch past the end exits at once (a few us), a replay costs a
@@ -1234,7 +1274,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             const int S = near_end ? kShort : kLong;
             hipError_t e = use_graph ? hipGraphLaunch(c->step_exec[near_end ? 1 : 0], c->stream) : enqueue_steps(S);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream);
+                e = enqueue_tail();
             if (e == hipSuccess)
                 e = hipStreamSynchronize(c->stream);
             if (e != hipSuccess) {
@@ -1343,30 +1383,21 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     unsigned long long *cnt = c->census.p;
     unsigned long long *cz = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
     int32_t *h_goal_end = reinterpret_cast<int32_t *>(c->h_stage + 128);
-    HIP_TRY(hipMemsetAsync(cnt, 0, 24, c->stream));
-    HIP_TRY(hipMemsetAsync(cnt + 3, 0xff, 16, c->stream));
-    hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt);
-    PA_TRY(check_launch());
-    HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
     c->walk_ready = false;
-    if (!sharded) {
-        // the backtrace walk rides on this round trip: pastar_gpu_alignment
-        // then needs no launch and no wait of its own
-        int total_len = 0;
-        uint16_t goal_pos[PASTAR_MAX_SEQ] = {0};
-        for (int i = 0; i < c->n; i++) {
-            total_len += c->hp.len[i];
-            goal_pos[i] = (uint16_t)c->hp.len[i];
-        }
-        PA_TRY(ensure_walk_buffers(c, total_len));
-        PA_TRY(enqueue_walk(c, goal_pos, total_len, false));
-        HIP_TRY(hipMemcpyAsync(c->h_walk + 4, c->walk_info.p, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->h_walk_masks, c->walk_masks.p, 4 * ((size_t)total_len + 1), hipMemcpyDeviceToHost,
-                               c->stream));
-        c->walk_ready = true;
+    if (sharded) {
+        HIP_TRY(hipMemsetAsync(cnt, 0, 24, c->stream));
+        HIP_TRY(hipMemsetAsync(cnt + 3, 0xff, 16, c->stream));
+        hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt, nullptr);
+        PA_TRY(check_launch());
+        HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(cz, cnt, 40, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    } else {
+        // the census, the goal and the backtrace walk came back with the
+        // last replay (the walk ran only if the goal was reached):
+        // pastar_gpu_alignment needs no launch and no wait of its own
+        c->walk_ready = h.status == 1;
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
     int goal_g = *h_goal_end;
     if (sharded) {
         int64_t mn[1] = {goal_g};
