@@ -1584,6 +1584,56 @@ __global__ void queue_reset_kernel(Queues *__restrict__ q, uint32_t *__restrict_
     q->R[b][sq] = 0;
 }
 
+// A search's device setup in one launch (in place of a table fill, a queue
+// reset and five small memsets): the node table cleared (init_table_kernel),
+// the queues reset (queue_reset_kernel's rule, when they are known
+// consistent), the step statistics, the arrival stamps, the goal and the
+// open-list census zeroed by block 0.
+template <int SW>
+__global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restrict__ table, uint64_t nslots, int kw,
+                                                            Queues *__restrict__ q, uint32_t *__restrict__ chunk_tab,
+                                                            unsigned long long maxch, int reset_queues,
+                                                            StepStats *__restrict__ stats,
+                                                            unsigned long long *__restrict__ stamps,
+                                                            int *__restrict__ goal,
+                                                            unsigned long long *__restrict__ census)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < nslots; i += stride) {
+        uint64_t *s = table + i * SW;
+#pragma unroll
+        for (int w = 0; w < SW; w++)
+            s[w] = w == kw ? ~0ull : (w == kw + 1 ? (uint64_t)kIntMax : 0ull);
+    }
+    if (reset_queues) {
+        for (uint64_t k = tid; k < (uint64_t)kBuckets * kSub; k += stride) {
+            const int b = (int)(k % kBuckets), sq = (int)(k / kBuckets);
+            const unsigned long long w = q->W[b][sq];
+            unsigned long long used = (w + kChunk - 1) >> kChunkLog2;
+            if (used > maxch)
+                used = maxch;
+            uint32_t *row = chunk_tab + ((size_t)b * kSub + sq) * maxch;
+            for (unsigned long long c = 0; c < used; c++)
+                row[c] = 0;
+            q->W[b][sq] = 0;
+            q->R[b][sq] = 0;
+        }
+    }
+    if (blockIdx.x == 0) {
+        unsigned long long *sw = reinterpret_cast<unsigned long long *>(stats);
+        for (int k = threadIdx.x; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
+            sw[k] = 0;
+        for (int k = threadIdx.x; k < kArrive; k += blockDim.x)
+            stamps[k] = 0;
+        if (threadIdx.x == 0) {
+            *goal = kIntMax;
+            census[0] = census[1] = census[2] = 0;
+            census[3] = census[4] = ~0ull;
+        }
+    }
+}
+
 // Open entries left in the queues (current or superseded), for the
 // statistics: one read of every cursor pair.
 // gate (may be null): run only when the search ended with the goal found

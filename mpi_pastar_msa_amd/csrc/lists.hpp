@@ -121,6 +121,11 @@ __global__ __launch_bounds__(kListThreads) void lists_dequeue_kernel(SearchArgs 
     if (b < 0)
         b = 0;
     int result_f = kIntMax;
+    if (tid == 0) {  // an empty OpenList never enters the bucket loop
+        taken_s = 0;
+        reopen_s = 0;
+    }
+    __syncthreads();
     for (; b < kBuckets; b++) {
         if (tid < kSub) {
             const unsigned long long r = ld_agent(&a.q->R[b][tid]), w = ld_agent(&a.q->W[b][tid]);

@@ -326,13 +326,13 @@ struct pastar_ctx {
     int learned_log2 = 0;
     // preallocated backtrace buffers (pastar_gpu_alignment)
     DevBuf<uint64_t> walk_key, walk_last;
+    DevBuf<uint64_t> walk_goal;  // the goal's key (the one-shard search's walk start)
     DevBuf<int32_t> walk_masks;
     DevBuf<int> walk_info;
     uint64_t *h_walk = nullptr;  // pinned: key in, {info, masks} out
     int32_t *h_walk_masks = nullptr;  // pinned: a walked stretch of parent masks
     size_t h_walk_masks_n = 0;
     unsigned char *h_stage = nullptr;  // pinned: per-search uploads (Ctl, origin record)
-    DevBuf<uint8_t> seed_rec;          // the origin record of a search
     DevBuf<unsigned long long> census;  // open-list census of a search
     unsigned char *h_gather = nullptr;  // pinned: a sharded step's gathered values
 };
@@ -898,7 +898,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         PA_TRY(c->chunk_tab.alloc((size_t)kBuckets * kSub * maxch));
         PA_TRY(c->pool.alloc((size_t)chunks * kChunk));
         PA_TRY(c->stats.alloc(1));
-        PA_TRY(c->ctl.alloc(1));
+        PA_TRY(c->ctl.alloc(2));  // the Ctl, then the search's origin record (one upload)
         PA_TRY(c->stamps.alloc(kArrive));
         PA_TRY(c->goal.alloc(1));
         if (c->tr) {
@@ -913,26 +913,29 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         c->cap_maxch = maxch;
         c->cap_outbox = cfg.outbox_cap;
     }
-    const int blocks = (int)std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock);
-    if (sw == 4)
-        hipLaunchKernelGGL((init_table_kernel<4>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
-    else
-        hipLaunchKernelGGL((init_table_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots, c->kw);
-    PA_TRY(check_launch());
+    if (!c->census.p)
+        PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
+    bool reset_queues = true;
     if (!same || !c->queues_clean_known) {
         // fresh buffers: clear everything once
         HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
         HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
         c->queues_clean_known = true;
-    } else {
-        // the chunk-table entries the previous search used, then the cursors
-        hipLaunchKernelGGL(queue_reset_kernel, dim3((kBuckets * kSub + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                           c->stream, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch);
-        PA_TRY(check_launch());
+        reset_queues = false;
     }
-    HIP_TRY(hipMemsetAsync(c->stats.p, 0, sizeof(StepStats), c->stream));
-    HIP_TRY(hipMemsetAsync(c->stamps.p, 0, sizeof(unsigned long long) * kArrive, c->stream));
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->goal.p, kIntMax, 1, c->stream));
+    // the table, the used chunk-table entries and cursors, the statistics,
+    // stamps, goal and census: one launch
+    const int blocks = (int)std::max<uint64_t>(
+        (kBuckets * kSub + kBlock - 1) / kBlock, std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock));
+    if (sw == 4)
+        hipLaunchKernelGGL((search_init_kernel<4>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
+                           c->kw, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch, reset_queues ? 1 : 0,
+                           c->stats.p, c->stamps.p, c->goal.p, c->census.p);
+    else
+        hipLaunchKernelGGL((search_init_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
+                           c->kw, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch, reset_queues ? 1 : 0,
+                           c->stats.p, c->stamps.p, c->goal.p, c->census.p);
+    PA_TRY(check_launch());
     return PASTAR_OK;
 }
 
@@ -1092,10 +1095,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
-    // uploads from pinned staging, stream-ordered (no host round trip
-    // before the first step)
+    // uploaded below together with the origin record, from pinned staging,
+    // stream-ordered (no host round trip before the first step)
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
-    HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
 
     SearchArgs a{};
     a.P = c->dP.p;
@@ -1137,9 +1139,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     // seed: the origin (Sequences::get_initial_node, Sequences.cpp:70-77) on
     // its owner shard, through the same relax path as remote records
     const int origin_owner = G > 1 ? owner_of(c->n, zero, G, c->hp.hash_type, c->hp.hash_shift) : 0;
-    if (!c->seed_rec.p)
-        PA_TRY(c->seed_rec.alloc(64));
-    uint8_t *drec = c->seed_rec.p;
+    uint8_t *drec = reinterpret_cast<uint8_t *>(c->ctl.p + 1);
     {
         std::vector<uint8_t> rec(rb, 0);
         uint64_t key[4];
@@ -1147,9 +1147,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::memcpy(rec.data(), key, 8 * KW);
         int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
         std::memcpy(rec.data() + 8 * KW, tail, 16);
-        unsigned char *stage = c->h_stage + ((sizeof(Ctl) + 63) / 64) * 64;
-        std::memcpy(stage, rec.data(), rb);
-        HIP_TRY(hipMemcpyAsync(drec, stage, rb, hipMemcpyHostToDevice, c->stream));
+        std::memcpy(c->h_stage + sizeof(Ctl), rec.data(), rb);
+        HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl) + rb, hipMemcpyHostToDevice, c->stream));
     }
     if (c->shard == origin_owner) {
         ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
@@ -1237,18 +1236,17 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             goal_pos[i] = (uint16_t)c->hp.len[i];
         }
         PA_TRY(ensure_walk_buffers(c, total_len));
-        if (!c->census.p)
-            PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
-        HIP_TRY(hipMemsetAsync(c->census.p, 0, 24, c->stream));
-        HIP_TRY(hipMemsetAsync(c->census.p + 3, 0xff, 16, c->stream));
-        pack_key(c, goal_pos, c->h_walk);
-        HIP_TRY(hipMemcpyAsync(c->walk_key.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+        if (!c->walk_goal.p) {  // the goal key, once per context (census zeroed by search_init_kernel)
+            PA_TRY(c->walk_goal.alloc(4));
+            pack_key(c, goal_pos, c->h_walk);
+            HIP_TRY(hipMemcpyAsync(c->walk_goal.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
+        }
         unsigned long long *cz_tail = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
         int32_t *goal_tail = reinterpret_cast<int32_t *>(c->h_stage + 128);
         const int *gate = &c->ctl.p->status;
         auto enqueue_tail = [&]() -> hipError_t {
             hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, c->census.p, gate);
-            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_key.p, total_len + 1, 0, c->walk_masks.p,
+            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_goal.p, total_len + 1, 0, c->walk_masks.p,
                      c->walk_last.p, c->walk_info.p, gate);
             hipError_t e = hipGetLastError();
             if (e == hipSuccess)
@@ -1384,9 +1382,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     unsigned long long *cz = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
     int32_t *h_goal_end = reinterpret_cast<int32_t *>(c->h_stage + 128);
     c->walk_ready = false;
-    if (sharded) {
-        HIP_TRY(hipMemsetAsync(cnt, 0, 24, c->stream));
-        HIP_TRY(hipMemsetAsync(cnt + 3, 0xff, 16, c->stream));
+    if (sharded) {  // (census zeroed by search_init_kernel)
         hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, cnt, nullptr);
         PA_TRY(check_launch());
         HIP_TRY(hipMemcpyAsync(h_goal_end, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream));
