@@ -408,3 +408,31 @@ def test_rccl_transport_world_one(name, kat):
         assert o_cost(kat, name, rows) == ref["score"]
         if "alignment_md5" in ref:
             assert hashlib.md5("".join(x + "\n" for x in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
+@pytest.mark.parametrize("gaps", [(35, 25, 30), (20, 40, 10)])
+def test_search_general_gap_form(gaps, kat):
+    """Whole searches under patched gap constants (Node.cpp:130-152's open /
+    extend / gap-gap branches, PairAlign's affine form).  With gap_open !=
+    gap_ext a node's g depends on its parent's mask when it was expanded, so
+    the reference's own search is order-dependent and its backtrace need not
+    cost its score (tests/test_oracle.py shows both on the oracle): no score
+    to match on general inputs.  What is checked: the search completes with
+    a valid alignment of the inputs, on the batched engine (the LDS-resident
+    search takes equal gap costs only), and on inputs whose optimal alignment
+    has no gaps (test2, PF08184) the score is the reference's."""
+    go, ge, gg = gaps
+    for name in ("test2", "PF08184"):
+        ref = kat["inputs"][name]
+        with Engine(Sequences.from_fasta(golden(ref["file"])), gap_open=go, gap_ext=ge, gap_gap=gg).init() as e:
+            r = e.pa_star(PAStarOpt())
+            assert r.solo == 0 and r.score == ref["score"]
+            assert [row.replace("-", "") for row in e.alignment()] == e.sequences.seqs
+    rng = random.Random(go * 7 + ge)
+    for trial in range(6):
+        n = 3 + trial % 3
+        seqs = ["".join(rng.choice("ACDEFGHIKLMNPQRSTVWY") for _ in range(rng.randint(3, 12))) for _ in range(n)]
+        with Engine(seqs, gap_open=go, gap_ext=ge, gap_gap=gg).init() as e:
+            r = e.pa_star(PAStarOpt())
+            assert r.score > 0
+            assert [row.replace("-", "") for row in e.alignment()] == seqs

@@ -167,3 +167,24 @@ def test_oracle_gap_constants_patchable(kat):
     kids = {k[3]: k for k, _ in other.get_neigh(((1,) * base.n, 0, 0, (1 << base.n) - 1))}
     kb = {k[3]: k for k, _ in base.get_neigh(((1,) * base.n, 0, 0, (1 << base.n) - 1))}
     assert kids.keys() == kb.keys()
+
+
+def test_unequal_gap_costs_make_the_search_order_dependent():
+    """Why the GPU test of patched gaps checks validity only: with gap_open !=
+    gap_ext the reference's g of a node depends on its parent's mask at
+    expansion time (Node.cpp:130-152), so its serial and threaded searches
+    reach different scores on some inputs, and a backtrace need not cost the
+    score.  With the reference's equal costs both hold."""
+    rng = random.Random(1)
+    differ = inconsistent = 0
+    for t in range(6):
+        seqs = ["".join(rng.choice("ACDEFGHIKLMNPQRSTVWY") for _ in range(rng.randint(3, 12)))
+                for _ in range(rng.randint(3, 5))]
+        o = orc.Oracle(seqs=seqs, gaps=(20, 40, 10))
+        a, m = o.astar(), o.pastar_mt(3)
+        differ += a["score"] != m["score"]
+        inconsistent += o.alignment_cost(a["rows"]) != a["score"]
+        oe = orc.Oracle(seqs=seqs)
+        ae = oe.astar()
+        assert ae["score"] == oe.pastar_mt(3)["score"] == oe.alignment_cost(ae["rows"])
+    assert differ + inconsistent >= 1
