@@ -435,7 +435,7 @@ struct Ctl {
     int fail_mask;  // kFail* bits of the capacity that ran out
     int has_work;   // select found a live bucket (multi-shard termination)
     int debug;      // 1: select validates its scan start (diagnostics)
-    int pad0;
+    int deep_blocks;  // block-rounds per continuation level across the chip (kDeepBlocks by default)
     unsigned long long kmax;
     unsigned long long pool_chunks, maxch;
     unsigned long long table_slots;
@@ -618,7 +618,7 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
 // the current batch's buckets are expanded by the same block in the same
 // launch, up to `depth` levels, instead of waiting for the next step.
 constexpr int kLocalCap = 128;
-constexpr int kDeepBlocks = 256;  // block-rounds per continuation level across the chip
+constexpr int kDeepBlocks = 1024;  // block-rounds per continuation level across the chip (profiles/r2_tune_deep_blocks.txt)
 // A continuation entry carries the parent as relaxed (key, g, h, mask), so
 // the next level needs no table read before it stages the pair terms.
 template <int KW>
@@ -1293,7 +1293,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // that the blocks together run about kDeepBlocks block-rounds per level
     // (a round costs ceil(2^N / 64) child passes)
     const int passes = masks > 64 ? masks / 64 : 1;
-    const unsigned long long rounds = (unsigned long long)kDeepBlocks / (nact * passes);
+    const unsigned long long rounds = (unsigned long long)ctl->deep_blocks / (nact * passes);
     const int depth = rounds >= (unsigned long long)ctl->deep_rounds ? view.depth : 1;
     const int f_limit = f0 + (int)(((long long)view.batch_b + view.batch_nb) << w);
     __shared__ LEntry<KW> lq[2][kLocalCap];

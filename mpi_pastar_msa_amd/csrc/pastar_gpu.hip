@@ -1095,6 +1095,10 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
+    {
+        const char *e = std::getenv("PASTAR_DEEP_BLOCKS");  // tuning override
+        hc.deep_blocks = e && *e ? std::max(1, std::atoi(e)) : kDeepBlocks;
+    }
     // uploaded below together with the origin record, from pinned staging,
     // stream-ordered (no host round trip before the first step)
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
@@ -1677,7 +1681,11 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     // levels per launch: the cheaper an expansion, the deeper (PF08184 0.40
     // -> 0.22 ms at 64, 2 launches; syn4x200 1.52 -> 1.44 ms at 12 with one
     // round; profiles/r1_depth_sweep.txt)
-    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 3 ? 64 : c->n == 4 ? 12 : 8);
+    // (round 2, with 1024 block-rounds per continuation level: N = 4 at 64
+    // levels is the best or tied on five 4 x 150..300 inputs, syn4x200 1.48
+    // -> 1.19 ms; N = 5, 6 at 8: kinase is best at 6..8, narrower inputs at
+    // 12..32; profiles/r2_tune_depth.txt)
+    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 4 ? 64 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     if (o.mode < PASTAR_MODE_AUTO || o.mode > PASTAR_MODE_SOLO)
