@@ -617,7 +617,10 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
 // Block-local continuation queue (LDS): improved children whose f lies in
 // the current batch's buckets are expanded by the same block in the same
 // launch, up to `depth` levels, instead of waiting for the next step.
-constexpr int kLocalCap = 128;
+#ifndef PASTAR_LOCAL_CAP
+#define PASTAR_LOCAL_CAP 128
+#endif
+constexpr int kLocalCap = PASTAR_LOCAL_CAP;
 constexpr int kDeepBlocks = 1024;  // block-rounds per continuation level across the chip (profiles/r2_tune_deep_blocks.txt)
 // A continuation entry carries the parent as relaxed (key, g, h, mask), so
 // the next level needs no table read before it stages the pair terms.

@@ -970,7 +970,10 @@ int estimate_band_log2(pastar_ctx *c, int h0, int64_t band_opt, int *w_out)
         // 1.9 -> 1.5 ms with fewer expansions, PF08184 61 expansions for 60
         // serial; syn8x400 tied at 1/8 and 1/4, syn8x100 24.5 ms at 1/4
         // against 29 at 1/8)
-        band = cnt ? std::max<int64_t>(1, sum / cnt / (c->n >= 7 ? 4 : 8)) : 1;
+        int div = c->n >= 7 ? 4 : 8;
+        if (const char *e = std::getenv("PASTAR_BAND_DIV"))  // tuning override
+            div = std::max(1, std::atoi(e));
+        band = cnt ? std::max<int64_t>(1, sum / cnt / div) : 1;
     }
     int w = 0;
     while ((2ll << w) <= band * 4 / 3 && w < 24)  // nearest power of two
@@ -1654,11 +1657,13 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         o = *opts;
     SearchCfg cfg;
     const unsigned long long masks = (1ull << c->n) - 1;
-    // most parents per step: 131072 up to N = 6 (kinase 20.2 -> 18.4 ms),
-    // 65536 beyond (syn8x400 72 ms at 65536, 73.5 at 131072)
+    // most parents per step: up to N = 6 see below; 65536 beyond (syn8x400
+    // 72 ms at 65536 and at 131072)
     if (o.batch_nodes > (1ll << 30))  // batch offsets are 32-bit on the device
         return fail(PASTAR_EINVAL, "batch_nodes %lld above 2^30", (long long)o.batch_nodes);
-    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : (c->n <= 6 ? 131072ull : 65536ull);
+    // (round 2: 262144 up to N = 6, kinase 16.7 -> 15.2 ms, narrower inputs
+    // flat; profiles/r2_tune_batch.txt)
+    cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : (c->n <= 6 ? 262144ull : 65536ull);
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     // default node-table size: learned from the last search on this context
     // (a repeated search of the same problem initialises only what it
