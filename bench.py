@@ -340,7 +340,7 @@ def main():
                 else "reference fixture %s" % fasta_name,
         "config": {"workload": args.workload, "baseline_config": cfg_desc, "n_seqs": n,
                    "lengths": [len(s) for s in seqs.seqs], "hash": "FZORDER/12",
-                   "batch_nodes": args.batch or (262144 if n <= 6 else 65536), "depth": args.depth or (64 if n <= 4 else 8),
+                   "batch_nodes": args.batch or (262144 if n <= 6 else 65536), "depth": args.depth or (128 if n <= 4 else 8),
                    "parallelism": "shard%d" % world},
         "score": score,
         "score_ok": score == known,

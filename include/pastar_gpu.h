@@ -111,7 +111,8 @@ typedef struct pastar_search_opts {
     int32_t depth;            /* expansion levels per step: children whose f
                                  falls in the step's buckets are expanded by
                                  the same workgroup in the same launch, up to
-                                 depth - 1 more levels (0 = default)       */
+                                 depth - 1 more levels (0 = default, at most
+                                 1024)                                     */
     int32_t mode;             /* PASTAR_MODE_*: which engine runs the search */
 } pastar_search_opts;
 

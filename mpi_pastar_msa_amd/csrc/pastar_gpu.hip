@@ -1681,16 +1681,16 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.verbose = o.verbose;
     cfg.profile = o.profile;
     cfg.eager = o.eager;
-    if (o.depth < 0 || o.depth > 64)
-        return fail(PASTAR_EINVAL, "depth %d outside [0, 64]", o.depth);
+    if (o.depth < 0 || o.depth > 1024)
+        return fail(PASTAR_EINVAL, "depth %d outside [0, 1024]", o.depth);
     // levels per launch: the cheaper an expansion, the deeper (PF08184 0.40
     // -> 0.22 ms at 64, 2 launches; syn4x200 1.52 -> 1.44 ms at 12 with one
     // round; profiles/r1_depth_sweep.txt)
-    // (round 2, with 1024 block-rounds per continuation level: N = 4 at 64
-    // levels is the best or tied on five 4 x 150..300 inputs, syn4x200 1.48
-    // -> 1.19 ms; N = 5, 6 at 8: kinase is best at 6..8, narrower inputs at
-    // 12..32; profiles/r2_tune_depth.txt)
-    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 4 ? 64 : 8);
+    // (round 2, with 1024 block-rounds per continuation level: N <= 4 at
+    // 128 levels is the best or tied on 4 of 5 inputs of 3..4 x 150..400,
+    // syn4x200 1.48 -> 1.17 ms; N = 5, 6 at 8: kinase is best at 6..12,
+    // narrower inputs at 12..32; profiles/r2_tune_depth.txt)
+    cfg.depth = o.depth > 0 ? o.depth : (c->n <= 4 ? 128 : 8);
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;
     if (o.mode < PASTAR_MODE_AUTO || o.mode > PASTAR_MODE_SOLO)
