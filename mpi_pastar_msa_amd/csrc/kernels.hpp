@@ -1591,7 +1591,9 @@ __global__ void queue_reset_kernel(Queues *__restrict__ q, uint32_t *__restrict_
 // reset and five small memsets): the node table cleared (init_table_kernel),
 // the queues reset (queue_reset_kernel's rule, when they are known
 // consistent), the step statistics, the arrival stamps, the goal and the
-// open-list census zeroed by block 0.
+// open-list census zeroed by block 0, which also copies the search's control
+// block and origin record from pinned host memory (`stage`, written by the
+// host before the launch; in place of a host-to-device copy).
 template <int SW>
 __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restrict__ table, uint64_t nslots, int kw,
                                                             Queues *__restrict__ q, uint32_t *__restrict__ chunk_tab,
@@ -1599,7 +1601,9 @@ __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restric
                                                             StepStats *__restrict__ stats,
                                                             unsigned long long *__restrict__ stamps,
                                                             int *__restrict__ goal,
-                                                            unsigned long long *__restrict__ census)
+                                                            unsigned long long *__restrict__ census,
+                                                            const uint32_t *__restrict__ stage,
+                                                            uint32_t *__restrict__ ctl_dst, int stage_words)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1624,6 +1628,8 @@ __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restric
         }
     }
     if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < stage_words; k += blockDim.x)
+            ctl_dst[k] = stage[k];
         unsigned long long *sw = reinterpret_cast<unsigned long long *>(stats);
         for (int k = threadIdx.x; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
             sw[k] = 0;
@@ -1700,13 +1706,11 @@ __global__ __launch_bounds__(kBlock) void open_census_kernel(SearchArgs a, int g
 // writing them to `masks`, until the origin, `max` steps, or (local_only) a
 // parent owned by another shard.  Single lane.  info = {steps, status}.
 template <int N, int KW>
-__global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table, uint64_t cap_mask,
-                            const uint64_t *__restrict__ start, int max, int local_only,
-                            int32_t *__restrict__ masks, uint64_t *__restrict__ last_key, int *__restrict__ info,
-                            const int *__restrict__ gate)
+__device__ __forceinline__ void walk_chain(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
+                                           uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
+                                           int local_only, int32_t *__restrict__ masks,
+                                           uint64_t *__restrict__ last_key, int *__restrict__ info)
 {
-    if (gate && *(volatile const int *)gate != 1)  // see queue_census_kernel
-        return;
     const DevProblem &Pg = *Pp;
     const int n = N ? N : Pg.n;
     constexpr int SW = slot_words<KW>();
@@ -1801,6 +1805,234 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
         last_key[w] = key[w];
     info[0] = steps;
     info[1] = status;
+}
+
+template <int N, int KW>
+__global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table, uint64_t cap_mask,
+                            const uint64_t *__restrict__ start, int max, int local_only,
+                            int32_t *__restrict__ masks, uint64_t *__restrict__ last_key, int *__restrict__ info,
+                            const int *__restrict__ gate)
+{
+    if (gate && *(volatile const int *)gate != 1)  // see queue_census_kernel
+        return;
+    walk_chain<N, KW>(Pp, table, cap_mask, start, max, local_only, masks, last_key, info);
+}
+
+// The backtrace walk two steps per memory round trip (one shard, 1-word keys,
+// 2 <= N <= 6; same result as walk_kernel with local_only = 0).  One wave:
+// lane 0 fetches the first probe line of the current node, and lane m
+// (1 <= m < 2^N) that of the node's candidate parent node - m.  The round
+// trip that returns the node's parent mask m0 then also holds the parent's
+// record (lane m0's line) and so the parent's own mask: the grandparent is
+// the next round's node.  A record missing from its first line (a displaced
+// key, rare at the table's load) is looked up along its probe chain.
+template <int N>
+__device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
+                                            uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
+                                            int32_t *__restrict__ masks, uint64_t *__restrict__ last_key,
+                                            int *__restrict__ info)
+{
+    static_assert(N >= 2 && N <= 6, "one lane per candidate parent");
+    constexpr int SW = slot_words<1>();
+    constexpr int LS = line_slots<1>();
+    const DevProblem &Pg = *Pp;
+    const KConst<N, 1> P = load_kconst<N, 1>(Pg);
+    const int lane = lane_id();
+    // this lane's key decrement (its candidate's coordinate offsets)
+    uint64_t dec = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if ((lane >> i) & 1)
+            dec += 1ull << P.kshift[i];
+    const uint64_t origin = Pg.origin_key[0];
+    uint64_t key = start[0];  // uniform
+    int steps = 0, status = 0;
+    // best of `k` along its whole probe chain (uniform; the rare path)
+    auto full_best = [&](uint64_t k, uint64_t &best) -> bool {
+        const uint64_t kk[1] = {k};
+        const int64_t s = lookup<1>(table, cap_mask, kk);
+        if (s < 0)
+            return false;
+        best = table[(uint64_t)s * SW + 1];
+        return true;
+    };
+    // the uniform key decrement of mask m
+    auto step_back = [&](uint64_t k, int m) -> uint64_t {
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if ((m >> i) & 1)
+                k -= 1ull << P.kshift[i];
+        return k;
+    };
+    for (;;) {
+        if (key == origin) {
+            status = 1;
+            break;
+        }
+        if (steps >= max) {
+            status = 2;
+            break;
+        }
+        int pos[N];
+        const uint64_t kk[1] = {key};
+        decode_key<N, 1>(P, N, kk, pos);
+        bool valid = lane < (1 << N);
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (((lane >> i) & 1) && pos[i] == 0)
+                valid = false;
+        const uint64_t ck = key - dec;  // lane 0: the node itself
+        uint64_t best = ~0ull;
+        bool found = false;
+        if (valid) {
+            const uint64_t ckk[1] = {ck};
+            const uint64_t *line = table + probe_start<1>(ckk, cap_mask) * SW;
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            u64x2 v[LS];
+#pragma unroll
+            for (int t = 0; t < LS; t++)
+                v[t] = *reinterpret_cast<const u64x2 *>(line + t * SW);  // key, best
+#pragma unroll
+            for (int t = 0; t < LS; t++)
+                if (!found && v[t].x == ck) {
+                    best = v[t].y;
+                    found = true;
+                }
+        }
+        const uint64_t hit = __ballot(found);
+        uint64_t b0 = __shfl(best, 0);
+        if (!(hit & 1ull) && !full_best(key, b0)) {
+            status = -1;
+            break;
+        }
+        const int m0 = (int)(uint32_t)b0;
+        if (lane == 0)
+            masks[steps] = m0;
+        steps++;
+        key = step_back(key, m0);
+        if (key == origin) {
+            status = 1;
+            break;
+        }
+        if (steps >= max) {
+            status = 2;
+            break;
+        }
+        uint64_t b1 = __shfl(best, m0 & 63);
+        if (!((hit >> (m0 & 63)) & 1ull) && !full_best(key, b1)) {
+            status = -1;
+            break;
+        }
+        const int m1 = (int)(uint32_t)b1;
+        if (lane == 0)
+            masks[steps] = m1;
+        steps++;
+        key = step_back(key, m1);
+    }
+    if (lane == 0) {
+        last_key[0] = key;
+        info[0] = steps;
+        info[1] = status;
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void walk2_kernel(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
+                                                   uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
+                                                   int32_t *__restrict__ masks, uint64_t *__restrict__ last_key,
+                                                   int *__restrict__ info, const int *__restrict__ gate)
+{
+    if (gate && *(volatile const int *)gate != 1)  // see queue_census_kernel
+        return;
+    walk2_chain<N>(Pp, table, cap_mask, start, max, masks, last_key, info);
+}
+
+// The end of a one-shard graph replay in one launch (in place of the census,
+// the walk and a pack of the results; each small launch costs ~4.5 us of
+// stream time even when it has nothing to do).  Not finished (status != 1):
+// block 0 writes the control block and the goal to pinned host memory.
+// Finished: blocks 1.. count the open list's queue entries
+// (queue_census_kernel), block 0's first wave walks the goal's parent chain
+// (walk2_chain, or walk_chain on one lane), and the last block to arrive
+// writes the control block, the goal, the census and the walk's {steps,
+// status} and masks to pinned host memory.
+struct TailArgs {
+    const DevProblem *P;
+    const uint64_t *table;
+    uint64_t cap_mask;
+    const uint64_t *goal_key;
+    int max;
+    int32_t *masks;
+    uint64_t *last_key;
+    int *info;
+    const Queues *q;
+    unsigned long long *census;
+    const Ctl *ctl;
+    const int *goal;
+    unsigned *arrive;  // zero between launches
+    Ctl *h_ctl;
+    int *h_goal;
+    unsigned long long *h_census;
+    int *h_info;
+    int32_t *h_masks;
+};
+
+__device__ __forceinline__ void tail_copy_ctl(const TailArgs &t)
+{
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(t.ctl);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(t.h_ctl);
+    for (int k = threadIdx.x; k < (int)(sizeof(Ctl) / 4); k += blockDim.x)
+        dst[k] = ld_agent(&src[k]);
+    if (threadIdx.x == 0)
+        *t.h_goal = ld_agent(t.goal);
+}
+
+template <int N, int KW>
+__global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
+{
+    if (ld_agent(&t.ctl->status) != 1) {
+        if (blockIdx.x == 0)
+            tail_copy_ctl(t);
+        return;
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 64) {
+            constexpr bool kTwo = KW == 1 && N >= 2 && N <= 6;
+            if constexpr (kTwo)
+                walk2_chain<kTwo ? N : 2>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key, t.info);
+            else if (threadIdx.x == 0)
+                walk_chain<N, KW>(t.P, t.table, t.cap_mask, t.goal_key, t.max, 0, t.masks, t.last_key, t.info);
+        }
+    } else {
+        unsigned long long s = 0;
+        const int stride = (gridDim.x - 1) * blockDim.x;
+        for (int k = (blockIdx.x - 1) * blockDim.x + threadIdx.x; k < kBuckets * kSub; k += stride)
+            s += t.q->W[k / kSub][k % kSub] - t.q->R[k / kSub][k % kSub];
+        s = wave_sum(s);
+        if (lane_id() == 0 && s)
+            atomicAdd(t.census, s);
+    }
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();  // the walk's masks and info, the census adds: visible to the last block
+        last = atomicAdd(t.arrive, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    __threadfence();
+    tail_copy_ctl(t);
+    if (threadIdx.x < 5)
+        t.h_census[threadIdx.x] = ld_agent(&t.census[threadIdx.x]);
+    const int steps = ld_agent(&t.info[0]);
+    if (threadIdx.x < 2)
+        t.h_info[threadIdx.x] = ld_agent(&t.info[threadIdx.x]);
+    const int n = steps < t.max ? steps : t.max;
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+        t.h_masks[k] = ld_agent(&t.masks[k]);
+    if (threadIdx.x == 0)
+        *t.arrive = 0;
 }
 
 template <int KW>

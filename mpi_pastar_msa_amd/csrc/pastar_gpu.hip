@@ -270,10 +270,9 @@ struct pastar_ctx {
     bool solo_failed = false;  // a solo search of this problem overflowed its LDS capacity
     bool solo_active = false;  // the last search ran on the solo path (its node table is solo_dump)
     unsigned solo_attr_done = 0;  // per N: dynamic LDS limit raised
-    DevBuf<uint8_t> solo_buf;     // SoloOut + backtrace masks
     DevBuf<uint64_t> solo_dump;   // the solo node table in the main slot layout
     int solo_cap_log2 = 0;
-    unsigned char *h_solo = nullptr;  // pinned copy of solo_buf
+    unsigned char *h_solo = nullptr;  // pinned: SoloOut + backtrace masks, written by the kernel
     size_t h_solo_n = 0;
     // host-driven OpenList / ClosedList session (lists.hpp)
     bool lists_ready = false;
@@ -311,8 +310,8 @@ struct pastar_ctx {
     // the captured step graph, reused while the search buffers (and so the
     // kernel arguments) stay the same: capture + instantiate + destroy cost
     // ~0.5 ms per search
-    hipGraph_t step_graph[2] = {nullptr, nullptr};
-    hipGraphExec_t step_exec[2] = {nullptr, nullptr};
+    hipGraph_t step_graph[4] = {nullptr, nullptr, nullptr, nullptr};  // runs of kStepRuns[g] launches
+    hipGraphExec_t step_exec[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<unsigned char> step_key;
     long long last_steps = 0;  // steps the last completed search took
     // per-problem search constants, computed once per context
@@ -329,6 +328,7 @@ struct pastar_ctx {
     DevBuf<uint64_t> walk_goal;  // the goal's key (the one-shard search's walk start)
     DevBuf<int32_t> walk_masks;
     DevBuf<int> walk_info;
+    DevBuf<unsigned> tail_arrive;  // tail_kernel's arrival counter (zero between launches)
     uint64_t *h_walk = nullptr;  // pinned: key in, {info, masks} out
     int32_t *h_walk_masks = nullptr;  // pinned: a walked stretch of parent masks
     size_t h_walk_masks_n = 0;
@@ -496,6 +496,7 @@ struct Ops {
     void (*walk)(hipStream_t, const DevProblem *, const uint64_t *, uint64_t, const uint64_t *, int, int, int32_t *,
                  uint64_t *, int *, const int *);
     void (*lookup)(hipStream_t, const uint64_t *, uint64_t, const uint64_t *, uint64_t *);
+    void (*tail)(hipStream_t, const TailArgs &);
 };
 
 template <int N, int KW>
@@ -517,14 +518,25 @@ struct Impl {
     static void walk(hipStream_t s, const DevProblem *P, const uint64_t *t, uint64_t cm, const uint64_t *start, int max,
                      int local, int32_t *masks, uint64_t *last, int *info, const int *gate)
     {
+        if constexpr (KW == 1 && N >= 2 && N <= 6) {
+            if (!local) {
+                hipLaunchKernelGGL((walk2_kernel<N>), dim3(1), dim3(64), 0, s, P, t, cm, start, max, masks, last, info,
+                                   gate);
+                return;
+            }
+        }
         hipLaunchKernelGGL((walk_kernel<N, KW>), dim3(1), dim3(1), 0, s, P, t, cm, start, max, local, masks, last, info,
                            gate);
+    }
+    static void tail(hipStream_t s, const TailArgs &t)
+    {
+        hipLaunchKernelGGL((tail_kernel<N, KW>), dim3(64), dim3(kBlock), 0, s, t);
     }
     static void lookup(hipStream_t s, const uint64_t *t, uint64_t cm, const uint64_t *key, uint64_t *out)
     {
         hipLaunchKernelGGL((lookup_kernel<KW>), dim3(1), dim3(1), 0, s, t, cm, key, out);
     }
-    static Ops ops() { return Ops{expand_api, expand, insert_remote, walk, lookup}; }
+    static Ops ops() { return Ops{expand_api, expand, insert_remote, walk, lookup, tail}; }
 };
 
 template <int KW>
@@ -666,7 +678,7 @@ void pastar_gpu_destroy(pastar_ctx *c)
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     c->tr.reset();
-    for (int gi = 0; gi < 2; gi++) {
+    for (int gi = 0; gi < 4; gi++) {
         if (c->step_exec[gi])
             (void)hipGraphExecDestroy(c->step_exec[gi]);
         if (c->step_graph[gi])
@@ -882,6 +894,17 @@ struct SearchCfg {
 unsigned long long maxch_of(const SearchCfg &cfg) { return (cfg.subqueue_entries + kChunk - 1) / kChunk; }
 unsigned long long pool_chunks_of(const SearchCfg &cfg) { return (cfg.pool_entries + kChunk - 1) / kChunk; }
 
+// The device address of pinned host memory (hipHostMalloc, the base of the
+// allocation), for kernels that write their results straight to the host.
+template <typename T, typename U>
+int host_alias(T *h, U **d)
+{
+    void *p = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&p, (void *)h, 0));
+    *d = reinterpret_cast<U *>(p);
+    return PASTAR_OK;
+}
+
 int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
 {
     const int sw = slot_words_rt(c->kw);
@@ -912,29 +935,43 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         c->cap_pool = chunks;
         c->cap_maxch = maxch;
         c->cap_outbox = cfg.outbox_cap;
+        c->queues_clean_known = false;
     }
     if (!c->census.p)
         PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
+    return PASTAR_OK;
+}
+
+// A search's device setup, stream-ordered: the table, the used chunk-table
+// entries and cursors, the statistics, stamps, goal and census, and the
+// control block (+ origin record) from the pinned staging area c->h_stage,
+// `stage_bytes` of it (the host fills it before this call): one launch.
+int init_search(pastar_ctx *c, const SearchCfg &cfg, size_t stage_bytes)
+{
+    const int sw = slot_words_rt(c->kw);
+    const unsigned long long maxch = maxch_of(cfg);
     bool reset_queues = true;
-    if (!same || !c->queues_clean_known) {
+    if (!c->queues_clean_known) {
         // fresh buffers: clear everything once
         HIP_TRY(hipMemsetAsync(c->queues.p, 0, sizeof(Queues), c->stream));
         HIP_TRY(hipMemsetAsync(c->chunk_tab.p, 0, sizeof(uint32_t) * c->chunk_tab.n, c->stream));
         c->queues_clean_known = true;
         reset_queues = false;
     }
-    // the table, the used chunk-table entries and cursors, the statistics,
-    // stamps, goal and census: one launch
+    uint32_t *stage = nullptr;
+    PA_TRY(host_alias(c->h_stage, &stage));
+    uint32_t *ctl_dst = reinterpret_cast<uint32_t *>(c->ctl.p);
+    const int words = (int)(stage_bytes / 4);
     const int blocks = (int)std::max<uint64_t>(
         (kBuckets * kSub + kBlock - 1) / kBlock, std::min<uint64_t>(8192, (c->nslots + kBlock - 1) / kBlock));
     if (sw == 4)
         hipLaunchKernelGGL((search_init_kernel<4>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
-                           c->kw, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch, reset_queues ? 1 : 0,
-                           c->stats.p, c->stamps.p, c->goal.p, c->census.p);
+                           c->kw, c->queues.p, c->chunk_tab.p, maxch, reset_queues ? 1 : 0, c->stats.p, c->stamps.p,
+                           c->goal.p, c->census.p, stage, ctl_dst, words);
     else
         hipLaunchKernelGGL((search_init_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
-                           c->kw, c->queues.p, c->chunk_tab.p, (unsigned long long)maxch, reset_queues ? 1 : 0,
-                           c->stats.p, c->stamps.p, c->goal.p, c->census.p);
+                           c->kw, c->queues.p, c->chunk_tab.p, maxch, reset_queues ? 1 : 0, c->stats.p, c->stamps.p,
+                           c->goal.p, c->census.p, stage, ctl_dst, words);
     PA_TRY(check_launch());
     return PASTAR_OK;
 }
@@ -1102,8 +1139,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         const char *e = std::getenv("PASTAR_DEEP_BLOCKS");  // tuning override
         hc.deep_blocks = e && *e ? std::max(1, std::atoi(e)) : kDeepBlocks;
     }
-    // uploaded below together with the origin record, from pinned staging,
-    // stream-ordered (no host round trip before the first step)
+    // staged with the origin record below; the setup launch copies both to
+    // the device, stream-ordered (no host round trip before the first step)
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
 
     SearchArgs a{};
@@ -1155,7 +1192,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
         std::memcpy(rec.data() + 8 * KW, tail, 16);
         std::memcpy(c->h_stage + sizeof(Ctl), rec.data(), rb);
-        HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl) + rb, hipMemcpyHostToDevice, c->stream));
+        PA_TRY(init_search(c, cfg, sizeof(Ctl) + rb));
     }
     if (c->shard == origin_owner) {
         ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
@@ -1176,11 +1213,13 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // until select reports termination; with profiling the expand kernel
         // times itself on the device clock (event nodes inside a graph cost
         // several microseconds per step)
-        // runs of steps captured as two graphs, 32 and 4 launches; the short
-        // one finishes a search whose length the previous search on this
-        // context predicts, so few launches run after termination (each
-        // would only read `status` and leave)
-        constexpr int kLong = 32, kShort = 4;
+        // runs of steps captured as graphs of 4, 8, 16 and 32 launches: a
+        // replay takes the shortest run that covers the steps the previous
+        // search on this context predicts are left (32 with no prediction), so
+        // a repeated search usually ends in one replay and few launches run
+        // after termination (each would only read `status` and leave)
+        constexpr int kRuns = 4;
+        constexpr int kStepRuns[kRuns] = {4, 8, 16, 32};
         auto enqueue_steps = [&](int S) -> hipError_t {
             for (int k = 0; k < S; k++)
                 ops.expand(expand_grid, blk, c->stream, a);
@@ -1193,8 +1232,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             const int extra[3] = {(int)expand_grid.x, c->n, KW};
             std::memcpy(key.data() + sizeof(SearchArgs), extra, sizeof(extra));
         }
-        if (use_graph && !(c->step_exec[0] && c->step_key == key)) {
-            for (int gi = 0; gi < 2; gi++) {
+        if (use_graph && c->step_key != key) {  // new arguments: drop the runs captured for the old ones
+            for (int gi = 0; gi < kRuns; gi++) {
                 if (c->step_exec[gi])
                     (void)hipGraphExecDestroy(c->step_exec[gi]);
                 if (c->step_graph[gi])
@@ -1202,33 +1241,35 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 c->step_exec[gi] = nullptr;
                 c->step_graph[gi] = nullptr;
             }
-            c->step_key.clear();
-            for (int gi = 0; gi < 2 && use_graph; gi++) {
-                hipGraph_t graph = nullptr;
-                hipGraphExec_t exec = nullptr;
-                hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
-                hipError_t e2 = e == hipSuccess ? enqueue_steps(gi == 0 ? kLong : kShort) : e;
-                hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
-                if (e2 == hipSuccess && e3 == hipSuccess)
-                    e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-                if (e2 != hipSuccess || e3 != hipSuccess) {
-                    if (exec)
-                        (void)hipGraphExecDestroy(exec);
-                    if (graph)
-                        (void)hipGraphDestroy(graph);
-                    (void)hipGetLastError();
-                    use_graph = false;
-                    if (cfg.verbose)
-                        std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
-                                     hipGetErrorString(e2 != hipSuccess ? e2 : e3));
-                } else {
-                    c->step_graph[gi] = graph;
-                    c->step_exec[gi] = exec;
-                }
-            }
-            if (use_graph)
-                c->step_key = key;
+            c->step_key = key;
         }
+        // a run is captured the first time it is needed
+        auto run_exec = [&](int gi) -> hipGraphExec_t {
+            if (!use_graph || c->step_exec[gi])
+                return c->step_exec[gi];
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
+            hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+            hipError_t e2 = e == hipSuccess ? enqueue_steps(kStepRuns[gi]) : e;
+            hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
+            if (e2 == hipSuccess && e3 == hipSuccess)
+                e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+            if (e2 != hipSuccess || e3 != hipSuccess) {
+                if (exec)
+                    (void)hipGraphExecDestroy(exec);
+                if (graph)
+                    (void)hipGraphDestroy(graph);
+                (void)hipGetLastError();
+                use_graph = false;
+                if (cfg.verbose)
+                    std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
+                                 hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+                return nullptr;
+            }
+            c->step_graph[gi] = graph;
+            c->step_exec[gi] = exec;
+            return exec;
+        };
         long long steps_before = 0;
         int rc = PASTAR_OK;
         // the end-of-search work rides behind every replay, gated on the
@@ -1248,36 +1289,56 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             pack_key(c, goal_pos, c->h_walk);
             HIP_TRY(hipMemcpyAsync(c->walk_goal.p, c->h_walk, 32, hipMemcpyHostToDevice, c->stream));
         }
-        unsigned long long *cz_tail = reinterpret_cast<unsigned long long *>(c->h_stage);  // pinned
-        int32_t *goal_tail = reinterpret_cast<int32_t *>(c->h_stage + 128);
-        const int *gate = &c->ctl.p->status;
+        // pinned host memory the tail writes into, by its device addresses
+        unsigned long long *d_cz_tail = nullptr;
+        int32_t *d_goal_tail = nullptr, *d_info = nullptr, *d_masks = nullptr;
+        Ctl *d_ctl = nullptr;
+        PA_TRY(host_alias(c->h_stage, &d_cz_tail));
+        d_goal_tail = reinterpret_cast<int32_t *>(reinterpret_cast<unsigned char *>(d_cz_tail) + 128);
+        PA_TRY(host_alias(c->h_ctl, &d_ctl));
+        PA_TRY(host_alias(c->h_walk, &d_info));
+        d_info += 8;  // h_walk[4..5]
+        PA_TRY(host_alias(c->h_walk_masks, &d_masks));
+        if (!c->tail_arrive.p) {
+            PA_TRY(c->tail_arrive.alloc(1));
+            HIP_TRY(hipMemsetAsync(c->tail_arrive.p, 0, sizeof(unsigned), c->stream));
+        }
+        TailArgs ta{};
+        ta.P = c->dP.p;
+        ta.table = c->table.p;
+        ta.cap_mask = c->nslots - 1;
+        ta.goal_key = c->walk_goal.p;
+        ta.max = total_len + 1;
+        ta.masks = c->walk_masks.p;
+        ta.last_key = c->walk_last.p;
+        ta.info = c->walk_info.p;
+        ta.q = c->queues.p;
+        ta.census = c->census.p;
+        ta.ctl = c->ctl.p;
+        ta.goal = c->goal.p;
+        ta.arrive = c->tail_arrive.p;
+        ta.h_ctl = d_ctl;
+        ta.h_goal = d_goal_tail;
+        ta.h_census = d_cz_tail;
+        ta.h_info = d_info;
+        ta.h_masks = d_masks;
         auto enqueue_tail = [&]() -> hipError_t {
-            hipLaunchKernelGGL(queue_census_kernel, dim3(64), blk, 0, c->stream, c->queues.p, c->census.p, gate);
-            ops.walk(c->stream, c->dP.p, c->table.p, c->nslots - 1, c->walk_goal.p, total_len + 1, 0, c->walk_masks.p,
-                     c->walk_last.p, c->walk_info.p, gate);
-            hipError_t e = hipGetLastError();
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(goal_tail, c->goal.p, 4, hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(cz_tail, c->census.p, 40, hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_walk + 4, c->walk_info.p, 8, hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_walk_masks, c->walk_masks.p, 4 * ((size_t)total_len + 1),
-                                   hipMemcpyDeviceToHost, c->stream);
-            return e;
+            ops.tail(c->stream, ta);
+            return hipGetLastError();
         };
         for (;;) {
-            // long runs until the predicted end is near, then short ones: a
-            // launch past the end exits at once (a few us), a replay costs a
-            // host round trip (~20 us), so a long run may overshoot the
-            // predicted end by up to 16 launches
-            constexpr int kOvershoot = 16;
-            const bool near_end = c->last_steps > 0 && steps_before + kLong > c->last_steps + kOvershoot;
-            const int S = near_end ? kShort : kLong;
-            hipError_t e = use_graph ? hipGraphLaunch(c->step_exec[near_end ? 1 : 0], c->stream) : enqueue_steps(S);
+            // a launch past the end exits at once (a few us), a replay costs
+            // a host round trip (~20 us): the shortest run covering the
+            // predicted remainder, the longest beyond it
+            int gi = kRuns - 1;
+            if (c->last_steps > 0) {
+                const long long left = c->last_steps - steps_before;
+                gi = 0;
+                while (gi < kRuns - 1 && kStepRuns[gi] < left)
+                    gi++;
+            }
+            hipGraphExec_t ex = run_exec(gi);
+            hipError_t e = ex ? hipGraphLaunch(ex, c->stream) : enqueue_steps(kStepRuns[gi]);
             if (e == hipSuccess)
                 e = enqueue_tail();
             if (e == hipSuccess)
@@ -1549,8 +1610,6 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     for (int i = 0; i < c->n; i++)
         total_len += c->hp.len[i];
     const size_t out_bytes = sizeof(SoloOut) + 4 * ((size_t)total_len + 1);
-    if (c->solo_buf.n < out_bytes)
-        PA_TRY(c->solo_buf.alloc(out_bytes));
     const size_t C = (size_t)1 << pl.a.cap_log2;
     if (c->solo_dump.n < 4 * C)
         PA_TRY(c->solo_dump.alloc(4 * C));
@@ -1567,8 +1626,12 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     a.P = c->dP.p;
     a.codes = c->dcodes.p;
     a.sub = c->dsub.p;
-    a.out = reinterpret_cast<SoloOut *>(c->solo_buf.p);
-    a.masks = reinterpret_cast<int32_t *>(c->solo_buf.p + sizeof(SoloOut));
+    // the result record and the path go straight to pinned host memory (no
+    // copy after the launch)
+    unsigned char *d_out = nullptr;
+    PA_TRY(host_alias(c->h_solo, &d_out));
+    a.out = reinterpret_cast<SoloOut *>(d_out);
+    a.masks = reinterpret_cast<int32_t *>(d_out + sizeof(SoloOut));
     a.dump = c->solo_dump.p;
     a.max_path = total_len + 1;
     a.max_levels = cfg.max_steps > 0 ? cfg.max_steps : (1ll << 40);
@@ -1587,7 +1650,6 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     const double t0 = now_s();
     HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(kSoloThreads), args, pl.lds, c->stream));
     PA_TRY(check_launch());
-    HIP_TRY(hipMemcpyAsync(c->h_solo, c->solo_buf.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const double t1 = now_s();
     SoloOut o;
@@ -2134,7 +2196,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     hc.table_slots = c->nslots;
     hc.cur_b = kBuckets;  // empty: appends lower it
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
-    HIP_TRY(hipMemcpyAsync(c->ctl.p, c->h_stage, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+    PA_TRY(init_search(c, cfg, sizeof(Ctl)));
     HIP_TRY(hipStreamSynchronize(c->stream));
     SearchArgs &a = c->lists_args;
     a = SearchArgs{};
