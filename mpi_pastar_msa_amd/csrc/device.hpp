@@ -117,6 +117,16 @@ struct Remote {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Broadcast from a wave-uniform lane (a ballot's leader): v_readlane into a
+// scalar register, where __shfl would take an LDS round trip (ds_bpermute)
+__device__ __forceinline__ int bcast_lane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ unsigned long long bcast_lane(unsigned long long v, int lane)
+{
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), lane);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x)
 {
     x ^= x >> 33;
@@ -177,7 +187,7 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
     unsigned long long base = 0;
     if (lane == leader)
         base = atomicAdd(counter, (unsigned long long)__popcll(mask));
-    base = __shfl(base, leader);
+    base = bcast_lane(base, leader);
     if (pred) {
         const unsigned long long idx = base + __popcll(mask & ((1ull << lane) - 1ull));
         if (idx < cap)
@@ -208,6 +218,7 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
 template <int KW, int PFS>
 struct SlotWords {
     uint64_t w[PFS][KW + 1];
+    uint32_t start;  // the key's probe start (its hash, computed once)
 };
 
 template <int KW, int PFS>
@@ -219,7 +230,11 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
     constexpr int SW = slot_words<KW>();
     improved = false;
     claimed = false;
-    uint64_t idx = probe_start<KW>(key, cap_mask);
+    uint64_t idx;
+    if (has_pre)
+        idx = pre.start;
+    else
+        idx = probe_start<KW>(key, cap_mask);
     int probe = 0;
     // the prefetched slots: skip those holding other keys (key word 0 set
     // and different), and start at the first empty or candidate one with
@@ -339,8 +354,10 @@ __device__ __forceinline__ SlotWords<KW, PFS> slot_prefetch(const uint64_t *__re
     static_assert(KW <= 2 && PFS <= line_slots<KW>() && (KW == 1 || PFS == 1),
                   "prefetch: one line of 1-word keys, or one slot of a 2-word key");
     constexpr int SW = slot_words<KW>();
-    const uint64_t *s0 = table + probe_start<KW>(key, cap_mask) * SW;
     SlotWords<KW, PFS> o;
+    const uint64_t start = probe_start<KW>(key, cap_mask);
+    o.start = (uint32_t)start;
+    const uint64_t *s0 = table + start * SW;
 #pragma unroll
     for (int t = 0; t < PFS; t++) {
         const uint64_t *s = s0 + t * SW;

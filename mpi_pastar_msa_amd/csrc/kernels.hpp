@@ -461,6 +461,9 @@ struct Ctl {
     unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
     unsigned long long body_ticks[12];  // profile: expand phases of block 0 (diagnostics)
     unsigned long long body_launches;
+    // profile (PASTAR_PHASE_TIMERS builds): per-block chain statistics,
+    // {blocks, sum levels, max levels, sum rounds, max rounds, max ticks}
+    unsigned long long blk_stats[6];
     int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step, pad1;
     unsigned long long dbg_w, dbg_r;
 };
@@ -591,7 +594,7 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
     uint64_t pending = __ballot(pred);
     while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
-        const int bl = __shfl(b, leader);
+        const int bl = bcast_lane(b, leader);
         const uint64_t m = __ballot(pred && b == bl) & pending;
         unsigned long long base = 0;
         if (lane == leader) {
@@ -607,7 +610,7 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
             }
 #endif
         }
-        base = __shfl(base, leader);
+        base = bcast_lane(base, leader);
         if ((m >> lane) & 1ull)
             queue_store(a, bl, sq, base + __popcll(m & ((1ull << lane) - 1ull)), e, st);
         pending &= ~m;
@@ -642,6 +645,14 @@ struct LocalPush {
 };
 
 constexpr int kOutCap = 1024;  // entries a block defers to its final append
+
+// A group leader's verdict (0, 1, 2) to every lane of its group, by two
+// ballots (no LDS round trip; the leader lane is per group, not uniform)
+__device__ __forceinline__ int group_verdict(int verdict, int leader_lane)
+{
+    const uint64_t one = __ballot(verdict == 1), two = __ballot(verdict == 2);
+    return ((two >> leader_lane) & 1ull) ? 2 : (int)((one >> leader_lane) & 1ull);
+}
 
 // Block barrier for LDS data only: outstanding global stores (closed marks,
 // queue entries) need not land before the block moves on.
@@ -687,7 +698,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
             int base = 0;
             if (lane == leader)
                 base = atomicAdd(lp.count, __popcll(mask));
-            base = __shfl(base, leader);
+            base = bcast_lane(base, leader);
             if (want) {
                 const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
                 if (pos < lp.cap) {
@@ -713,7 +724,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
             int base = 0;
             if (lane == leader)
                 base = atomicAdd(lp.out_n, __popcll(mask));
-            base = __shfl(base, leader);
+            base = bcast_lane(base, leader);
             if (global) {
                 const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
                 if (pos < kOutCap) {
@@ -1048,7 +1059,7 @@ __device__ __forceinline__ int batch_range(uint32_t pf_lo, uint32_t pf_hi, unsig
     const int lane = lane_id();
     int r = 0;
     for (int g = 0; g < npw; g++) {
-        const unsigned long long ig = __shfl(i, g * lpn);
+        const unsigned long long ig = bcast_lane(i, g * lpn);
         const int cnt = __popcll(__ballot(pf_lo <= ig)) + __popcll(__ballot(pf_hi <= ig));
         if (lane / lpn == g)
             r = cnt - 1;
@@ -1191,7 +1202,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 verdict = (int)(uint32_t)aux != kIntMax ? 2 : 1;
                 *closed = par_.g;
             }
-            verdict = __shfl(verdict, leader_lane);
+            verdict = group_verdict(verdict, leader_lane);
             ok = verdict != 0;
             if (glane == 0) {
                 expanded += ok;
@@ -1242,7 +1253,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 verdict = (int)(uint32_t)laux != kIntMax ? 2 : 1;
                 *closed = par_.g;
             }
-            verdict = __shfl(verdict, leader_lane);
+            verdict = group_verdict(verdict, leader_lane);
             if (glane == 0) {
                 expanded += verdict != 0;
                 reopen += verdict == 2;
@@ -1288,6 +1299,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         BPHASE(7)
     };
 
+#ifdef PASTAR_PHASE_TIMERS
+    const unsigned long long blk_t0 = device_clock();
+    unsigned blk_levels = 1, blk_rounds = 0;
+#define BLK_COUNT(lv, rd) \
+    {                     \
+        blk_levels += lv; \
+        blk_rounds += rd; \
+    }
+#else
+#define BLK_COUNT(lv, rd)
+#endif
     // level 0: this block's share of the batch; levels 1..depth-1: the
     // children it queued in LDS (double-buffered)
     // continuation only while the batch leaves most of the chip idle (with
@@ -1339,6 +1361,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if (nn < nb)
             e_nx = batch_entry_at(a, view, prefix, bstart, nn, r);
         process(ok, e, ps, no_le, false, lp);
+        BLK_COUNT(0, 1)
     }
     // the continuation queue and the deferred entries are block-wide: one
     // barrier per level, after all of its chunks
@@ -1359,7 +1382,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             const int idx = base + wave * npw + group;
             const bool ok = idx < cnt;
             process(ok, Entry{0, 0}, no_ps, ok ? lq[cur][idx] : no_le, true, lq_next);
+            BLK_COUNT(0, 1)
         }
+        BLK_COUNT(1, 0)
         lds_barrier();
         BPHASE(3)
         cur = nxt;
@@ -1434,6 +1459,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if (stale)
             atomicAdd(&row[kStDropped], stale);
     }
+#ifdef PASTAR_PHASE_TIMERS
+    if ((view.timing & 4) && timing && threadIdx.x == 0) {
+        const unsigned long long dt = device_clock() - blk_t0;
+        atomicAdd(&ctl->blk_stats[0], 1ull);
+        atomicAdd(&ctl->blk_stats[1], (unsigned long long)blk_levels);
+        atomicMax(&ctl->blk_stats[2], (unsigned long long)blk_levels);
+        atomicAdd(&ctl->blk_stats[3], (unsigned long long)blk_rounds);
+        atomicMax(&ctl->blk_stats[4], (unsigned long long)blk_rounds);
+        atomicMax(&ctl->blk_stats[5], dt);
+    }
+#endif
+#undef BLK_COUNT
     const bool fuse = ctl->fuse;
     if (!fuse && !timing)
         return;
@@ -1900,7 +1937,7 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
                 }
         }
         const uint64_t hit = __ballot(found);
-        uint64_t b0 = __shfl(best, 0);
+        uint64_t b0 = bcast_lane((unsigned long long)best, 0);
         if (!(hit & 1ull) && !full_best(key, b0)) {
             status = -1;
             break;
@@ -1918,7 +1955,7 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
             status = 2;
             break;
         }
-        uint64_t b1 = __shfl(best, m0 & 63);
+        uint64_t b1 = bcast_lane((unsigned long long)best, m0 & 63);
         if (!((hit >> (m0 & 63)) & 1ull) && !full_best(key, b1)) {
             status = -1;
             break;

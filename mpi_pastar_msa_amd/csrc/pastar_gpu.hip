@@ -1514,7 +1514,10 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::fprintf(stderr, "\n[pastar] expand phases of block 0 (us/launch):");
         for (int k = 0; k < 10; k++)
             std::fprintf(stderr, " %.2f", (double)h.body_ticks[k] * 1e-2 / std::max<double>(1.0, (double)h.body_launches));
-        std::fprintf(stderr, "\n");
+        const double nb = std::max<double>(1.0, (double)h.blk_stats[0]);
+        std::fprintf(stderr, "\n[pastar] blocks %llu over %llu launches: levels mean %.1f max %llu, rounds mean %.1f max %llu, "
+                     "longest block %.2f us\n", h.blk_stats[0], h.body_launches, h.blk_stats[1] / nb, h.blk_stats[2],
+                     h.blk_stats[3] / nb, h.blk_stats[4], h.blk_stats[5] * 1e-2);
     }
     res->gap_ms = (double)h.gap_ticks * 1e-5;
     res->expand_launches = launches;
