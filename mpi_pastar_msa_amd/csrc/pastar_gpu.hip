@@ -653,6 +653,13 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
     PA_TRY(setup_problem(c.get(), p));
+    {
+        // load the code object now (the runtime loads it at the first use of
+        // one of its kernels): a context's first search then pays only its
+        // own setup (tools/gpu/cold_probe.py)
+        hipFuncAttributes fa;
+        HIP_TRY(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&h_kernel)));
+    }
     if (n_shards > 1 || rccl_id) {
         if (!rccl_id)
             return fail(PASTAR_EINVAL, "rccl_id required for n_shards > 1");
@@ -909,34 +916,49 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
 {
     const int sw = slot_words_rt(c->kw);
     const unsigned long long maxch = maxch_of(cfg), chunks = pool_chunks_of(cfg);
-    const bool same = c->table.p && c->cap_log2 == cfg.table_log2 && c->cap_kmax == cfg.kmax &&
-                      c->cap_pool == chunks && c->cap_maxch == maxch && c->cap_outbox == cfg.outbox_cap;
-    if (!same) {
-        c->table.reset();  // free before allocating the next set
+    // buffers are kept across searches and only ever grow: a search sized
+    // smaller than the last one (learned_log2) uses the front of the same
+    // table and pool, so its device addresses, and the step graphs captured
+    // for them, stay valid
+    const size_t table_words = ((size_t)1 << cfg.table_log2) * sw;
+    if (c->table.n < table_words) {
+        c->table.reset();  // free before allocating the larger one
+        PA_TRY(c->table.alloc(table_words));
+    }
+    c->nslots = 1ull << cfg.table_log2;
+    if (c->pool.n < (size_t)chunks * kChunk) {
         c->pool.reset();
-        c->chunk_tab.reset();
-        c->nslots = 1ull << cfg.table_log2;
-        PA_TRY(c->table.alloc((size_t)c->nslots * sw));
-        PA_TRY(c->queues.alloc(1));
-        PA_TRY(c->chunk_tab.alloc((size_t)kBuckets * kSub * maxch));
         PA_TRY(c->pool.alloc((size_t)chunks * kChunk));
+    }
+    if (!c->chunk_tab.p || c->cap_maxch != maxch) {  // the chunk table's row stride is maxch
+        c->chunk_tab.reset();
+        PA_TRY(c->chunk_tab.alloc((size_t)kBuckets * kSub * maxch));
+        c->queues_clean_known = false;
+    }
+    if (!c->queues.p) {
+        PA_TRY(c->queues.alloc(1));
         PA_TRY(c->stats.alloc(1));
         PA_TRY(c->ctl.alloc(2));  // the Ctl, then the search's origin record (one upload)
         PA_TRY(c->stamps.alloc(kArrive));
         PA_TRY(c->goal.alloc(1));
-        if (c->tr) {
-            const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
-            PA_TRY(c->outbox.alloc(bytes));
-            PA_TRY(c->inbox.alloc(bytes));
-            PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
-        }
-        c->cap_log2 = cfg.table_log2;
-        c->cap_kmax = cfg.kmax;
-        c->cap_pool = chunks;
-        c->cap_maxch = maxch;
-        c->cap_outbox = cfg.outbox_cap;
         c->queues_clean_known = false;
     }
+    if (c->tr) {
+        const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
+        if (c->outbox.n < bytes) {
+            c->outbox.reset();
+            c->inbox.reset();
+            PA_TRY(c->outbox.alloc(bytes));
+            PA_TRY(c->inbox.alloc(bytes));
+        }
+        if (!c->xcounts.p)
+            PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
+    }
+    c->cap_log2 = cfg.table_log2;
+    c->cap_kmax = cfg.kmax;
+    c->cap_pool = chunks;
+    c->cap_maxch = maxch;
+    c->cap_outbox = cfg.outbox_cap;
     if (!c->census.p)
         PA_TRY(c->census.alloc(5));  // entries left; debug: live, live below the goal, min f, min bucket
     return PASTAR_OK;
@@ -1732,11 +1754,13 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     // default node-table size: learned from the last search on this context
     // (a repeated search of the same problem initialises only what it
-    // needs), else 2^22 slots
-    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : (c->learned_log2 > 0 ? c->learned_log2 : 22);
+    // needs), else 2^24 slots (512 MB, cleared in ~0.1 ms: kinase's first
+    // search then runs without a capacity restart; tools/gpu/cold_probe.py)
+    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : (c->learned_log2 > 0 ? c->learned_log2 : 24);
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
-    cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 24);
+    // (the pool is never cleared: its size costs memory only, 2 GB here)
+    cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 28);
     cfg.subqueue_entries = o.subqueue_entries > 0 ? (unsigned long long)o.subqueue_entries : (1ull << 20);
     cfg.outbox_cap = std::max<unsigned long long>(1ull << 16, cfg.kmax * masks / std::max(1, c->n_shards));
     cfg.table_log2 = std::max(cfg.table_log2, c->grown_log2);
@@ -1796,12 +1820,13 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         }
         if (!mask)
             break;
+        // a restart repeats the search up to the failure: grow by 16x
         if (mask & kFailNear)
-            cfg.pool_entries *= 4;
+            cfg.pool_entries *= 16;
         if (mask & kFailFar)
             cfg.subqueue_entries *= 4;
         if (mask & kFailTable)
-            cfg.table_log2 = std::min(32, cfg.table_log2 + 2);
+            cfg.table_log2 = std::min(32, cfg.table_log2 + 4);
         if (mask & kFailOut)
             cfg.outbox_cap *= 4;
         c->grown_pool = cfg.pool_entries;

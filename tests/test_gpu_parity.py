@@ -197,6 +197,25 @@ def test_capacity_autogrow(kat):
             e2.pa_star(PAStarOpt(table_slots_log2=10, pool_entries=4096, autogrow=False))
 
 
+def test_buffers_grow_only_across_searches(kat):
+    """Search buffers are kept and only grow: a search sized below the last
+    one runs in the front of the same table and pool (and its captured step
+    graphs), a larger one reallocates; every search stays exact."""
+    ref = kat["inputs"]["syn4x200_s1"]
+    with _engine("syn4x200_s1", kat) as e:
+        md5s = []
+        for lg, pool in [(22, 1 << 24), (18, 1 << 20), (18, 1 << 20), (23, 1 << 25), (17, 1 << 22)]:
+            e.init()
+            r = e.pa_star(PAStarOpt(table_slots_log2=lg, pool_entries=pool, batch_nodes=65536, mode="batched"))
+            assert r.score == ref["score"] and r.capacity_retries == 0
+            assert r.table_slots == 1 << lg
+            rows = e.alignment()
+            md5s.append(hashlib.md5("".join(x + "\n" for x in rows).encode()).hexdigest())
+        assert len(set(md5s)) == 1
+        if "alignment_md5" in ref:
+            assert md5s[0] == ref["alignment_md5"]
+
+
 @pytest.mark.parametrize("name,shards", [("test2", 2), ("PF08184", 3), ("syn4x200_s1", 2), ("syn4x200_s1", 4),
                                           ("kinase", 4), ("syn8x100_s3", 8)])
 def test_sharded_search_one_gpu(name, shards, kat, oracles):
