@@ -104,8 +104,13 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
     extern __shared__ int lds[];
     int *bval = lds;                                              // [kPaWaves][L2 + 1] band top rows
     int *sub = bval + kPaWaves * W;                               // [alpha * alpha] when staged
-    volatile int *progress = sub + (SUB_LDS ? alpha * alpha : 0);  // [kPaWaves] band << 16 | steps done
-    uint8_t *bdir = (uint8_t *)(progress + kPaWaves);             // [kPaWaves][L2 + 1]
+    // [kPaWaves] band << 16 | steps done: an LDS-qualified pointer with
+    // workgroup-scope atomics, so the handshake is ds_read / ds_write (a
+    // volatile generic pointer compiles to flat accesses, and the wait after
+    // each flat store then also waits for the chunk's HBM stores)
+    typedef __attribute__((address_space(3))) int lds_int;
+    lds_int *progress = (lds_int *)(sub + (SUB_LDS ? alpha * alpha : 0));
+    uint8_t *bdir = (uint8_t *)(sub + (SUB_LDS ? alpha * alpha : 0) + kPaWaves);  // [kPaWaves][L2 + 1]
     uint8_t *s2 = bdir + kPaWaves * W;                            // [L2 + 1] codes of sequence y
     for (int k = threadIdx.x; k <= L2; k += blockDim.x)
         s2[k] = s2g[k];
@@ -113,7 +118,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
         for (int k = threadIdx.x; k < alpha * alpha; k += blockDim.x)
             sub[k] = WEIGHTED ? P.sub[k] * wgt : P.sub[k];
     if (threadIdx.x < kPaWaves)
-        progress[threadIdx.x] = -1;
+        __hip_atomic_store(&progress[threadIdx.x], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int32_t *subp;
     if constexpr (SUB_LDS)
         subp = sub;
@@ -133,8 +138,8 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
         const uint8_t *belowd = bdir + ((band + kPaWaves - 1) % kPaWaves) * W;
         int *top = bval + (band % kPaWaves) * W;
         uint8_t *topd = bdir + (band % kPaWaves) * W;
-        volatile int *prev_progress = progress + (band + kPaWaves - 1) % kPaWaves;
-        volatile int *my_progress = progress + band % kPaWaves;
+        lds_int *prev_progress = progress + (band + kPaWaves - 1) % kPaWaves;
+        lds_int *my_progress = progress + band % kPaWaves;
         int32_t *Mrow = M + (int64_t)(row_ok ? i : 0) * W;
         int2 *Crow = C + (int64_t)(row_ok ? i : 0) * W;
         // EQ_GAPS: the cells past the last row and column are +inf, so the
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 // lane 63 reads column L2 - t of band - 1's top row, written
                 // by its lane 0 at its step t + 63; one check covers 8 steps
                 const int need = ((band - 1) << 16) | (t0 + 71 < nsteps ? t0 + 71 : nsteps);
-                while (*prev_progress < need)
+                while (__hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
                     __builtin_amdgcn_s_sleep(1);
                 asm volatile("" ::: "memory");  // the row reads below stay after the wait
             }
@@ -257,7 +262,11 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                             topd[jj] = (uint8_t)tbd[u];
                     }
                 }
-                *my_progress = (band << 16) | (t0 + kPaChunk < nsteps ? t0 + kPaChunk : nsteps);
+                // the row's LDS writes stay before the publication (a wave's
+                // LDS operations complete in order)
+                asm volatile("" ::: "memory");
+                __hip_atomic_store(my_progress, (band << 16) | (t0 + kPaChunk < nsteps ? t0 + kPaChunk : nsteps),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             // the chunk's cells of this lane's row are columns j0 - 7 .. j0
             const int jlo = j0 - (kPaChunk - 1);
