@@ -1820,13 +1820,14 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         }
         if (!mask)
             break;
-        // a restart repeats the search up to the failure: grow by 16x
+        // a restart repeats the search up to the failure: the pool (memory
+        // only) grows by 16x, the table (cleared by every search) by 4x
         if (mask & kFailNear)
             cfg.pool_entries *= 16;
         if (mask & kFailFar)
             cfg.subqueue_entries *= 4;
         if (mask & kFailTable)
-            cfg.table_log2 = std::min(32, cfg.table_log2 + 4);
+            cfg.table_log2 = std::min(32, cfg.table_log2 + 2);
         if (mask & kFailOut)
             cfg.outbox_cap *= 4;
         c->grown_pool = cfg.pool_entries;
@@ -1848,6 +1849,9 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         while (lg < 32 && (1ull << lg) < want)
             lg++;
         c->learned_log2 = lg;
+        // a table grown past this search's need (25% load) is not kept as
+        // the floor of later searches: each one clears its whole table
+        c->grown_log2 = std::min(c->grown_log2, lg);
         c->grown_pool = std::max(c->grown_pool, c->last_pool_chunks * (unsigned long long)kChunk * 3 / 2);
         res->capacity_retries = retries;
         res->table_slots = (int64_t)c->nslots;
