@@ -2021,7 +2021,18 @@ struct TailArgs {
     unsigned long long *h_census;
     int *h_info;
     int32_t *h_masks;
+    uint32_t *h_done;  // set to `ticket` after everything above is in host memory
+    uint32_t ticket;
 };
+
+__device__ __forceinline__ void tail_done(const TailArgs &t)
+{
+    __syncthreads();  // the block's host writes issued
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(t.h_done, t.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 __device__ __forceinline__ void tail_copy_ctl(const TailArgs &t)
 {
@@ -2037,8 +2048,10 @@ template <int N, int KW>
 __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
 {
     if (ld_agent(&t.ctl->status) != 1) {
-        if (blockIdx.x == 0)
+        if (blockIdx.x == 0) {
             tail_copy_ctl(t);
+            tail_done(t);
+        }
         return;
     }
     if (blockIdx.x == 0) {
@@ -2079,6 +2092,7 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
         t.h_masks[k] = ld_agent(&t.masks[k]);
     if (threadIdx.x == 0)
         *t.arrive = 0;
+    tail_done(t);
 }
 
 template <int KW>

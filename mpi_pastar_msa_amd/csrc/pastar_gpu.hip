@@ -273,6 +273,8 @@ struct pastar_ctx {
     DevBuf<uint64_t> solo_dump;   // the solo node table in the main slot layout
     int solo_cap_log2 = 0;
     unsigned char *h_solo = nullptr;  // pinned: SoloOut + backtrace masks, written by the kernel
+    uint32_t solo_ticket = 0;         // the completion word's value of the last solo launch
+    uint32_t tail_ticket = 0;         // the same for the one-shard replay tail (tail_kernel)
     size_t h_solo_n = 0;
     // host-driven OpenList / ClosedList session (lists.hpp)
     bool lists_ready = false;
@@ -1344,9 +1346,34 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         ta.h_census = d_cz_tail;
         ta.h_info = d_info;
         ta.h_masks = d_masks;
+        // the completion word after the Ctl copy in h_ctl's pinned scratch
+        volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(reinterpret_cast<unsigned char *>(c->h_ctl) +
+                                                                        sizeof(Ctl) + 32);
+        ta.h_done = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(d_ctl) + sizeof(Ctl) + 32);
         auto enqueue_tail = [&]() -> hipError_t {
+            ta.ticket = ++c->tail_ticket;
+            *done = 0;
             ops.tail(c->stream, ta);
             return hipGetLastError();
+        };
+        // wait for a replay by watching the tail's completion word (its last
+        // store) rather than for the stream's completion signal; the stream is
+        // polled too, so a failure ends the wait with its error
+        auto wait_tail = [&]() -> hipError_t {
+            for (unsigned spin = 1; *done != ta.ticket; spin++) {
+                if ((spin & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(c->stream);
+                    if (q == hipSuccess && *done == ta.ticket)
+                        break;
+                    if (q != hipErrorNotReady) {
+                        const hipError_t e = hipStreamSynchronize(c->stream);
+                        if (e != hipSuccess)
+                            return e;
+                        return *done == ta.ticket ? hipSuccess : hipErrorUnknown;
+                    }
+                }
+            }
+            return hipSuccess;
         };
         for (;;) {
             // a launch past the end exits at once (a few us), a replay costs
@@ -1364,7 +1391,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             if (e == hipSuccess)
                 e = enqueue_tail();
             if (e == hipSuccess)
-                e = hipStreamSynchronize(c->stream);
+                e = wait_tail();
             if (e != hipSuccess) {
                 rc = fail(PASTAR_ENODEV, "search steps failed: %s", hipGetErrorString(e));
                 break;
@@ -1381,6 +1408,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         }
         if (h.status == 1)
             c->last_steps = h.steps;
+        else if (rc == PASTAR_OK)  // a failed search may be retried on regrown buffers: drain first
+            HIP_TRY(hipStreamSynchronize(c->stream));
         c->graph_used = use_graph;
         PA_TRY(rc);
     } else {
@@ -1634,7 +1663,9 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     int total_len = 0;
     for (int i = 0; i < c->n; i++)
         total_len += c->hp.len[i];
-    const size_t out_bytes = sizeof(SoloOut) + 4 * ((size_t)total_len + 1);
+    // SoloOut, the path's masks, then the completion word
+    const size_t done_off = (sizeof(SoloOut) + 4 * ((size_t)total_len + 1) + 63) & ~(size_t)63;
+    const size_t out_bytes = done_off + 64;
     const size_t C = (size_t)1 << pl.a.cap_log2;
     if (c->solo_dump.n < 4 * C)
         PA_TRY(c->solo_dump.alloc(4 * C));
@@ -1657,6 +1688,10 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     PA_TRY(host_alias(c->h_solo, &d_out));
     a.out = reinterpret_cast<SoloOut *>(d_out);
     a.masks = reinterpret_cast<int32_t *>(d_out + sizeof(SoloOut));
+    a.done = reinterpret_cast<uint32_t *>(d_out + done_off);
+    a.ticket = ++c->solo_ticket;
+    volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(c->h_solo + done_off);
+    *done = 0;  // (a fresh allocation holds anything)
     a.dump = c->solo_dump.p;
     a.max_path = total_len + 1;
     a.max_levels = cfg.max_steps > 0 ? cfg.max_steps : (1ll << 40);
@@ -1675,7 +1710,22 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     const double t0 = now_s();
     HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(kSoloThreads), args, pl.lds, c->stream));
     PA_TRY(check_launch());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // wait by watching the completion word (the kernel's last store) rather
+    // than for the stream's completion signal, a few microseconds later; the
+    // stream is still polled, so a failed launch ends the wait with its error
+    for (unsigned spin = 1; *done != a.ticket; spin++) {
+        if ((spin & 255) == 0) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess && *done == a.ticket)
+                break;
+            if (q != hipErrorNotReady) {
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                if (*done != a.ticket)
+                    return fail(PASTAR_ENODEV, "LDS-resident search ended without its result");
+                break;
+            }
+        }
+    }
     const double t1 = now_s();
     SoloOut o;
     std::memcpy(&o, c->h_solo, sizeof(o));

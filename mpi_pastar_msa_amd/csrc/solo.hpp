@@ -67,6 +67,8 @@ struct SoloArgs {
     int cap_log2, max_path, hc_cells, codes_len, alpha2;
     int off_prob, off_sub, off_codes, off_keys, off_best, off_hcl, off_open, off_batch, off_subw;  // LDS bytes
     int band_log2;  // < 0: the engine's automatic band (pastar_gpu.hip estimate_band_log2)
+    uint32_t *done;  // pinned host word: set to `ticket` after every result is written
+    uint32_t ticket;
 };
 
 // Wave-wide reductions on DPP lane moves (no LDS round trip): an inclusive
@@ -708,6 +710,10 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
             o.phase[k] = 0;
 #endif
         *a.out = o;
+        // the host may stop waiting as soon as it sees the ticket: the
+        // result and the path are in host memory before it (system fence)
+        __threadfence_system();
+        __hip_atomic_store(a.done, a.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
