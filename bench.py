@@ -52,6 +52,11 @@ WORKLOADS = {  # name -> (fasta fixture, BASELINE.json config it stands for, kno
 # serial (-t 1) expansion counts of the reference, for the useful rate
 SERIAL_EXPANSIONS = {"syn4x200_s1": 22089, "PF08184": 60, "kinase": 4497279}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+# measured on one MI355X (tools/micro/atomic_rate.hip, profiles/r2_atomic_rate.txt):
+# random 8-B loads over a 2 GB array, and random device-scope 8-B atomics
+# (18.4 G/s over 2 GB, 27 G/s over 256 MB)
+RANDOM_LOAD_PEAK_GS = 52.0
+RANDOM_ATOMIC_PEAK_GS = 18.4
 # the reference's own PF08184 run at -t 1: 60 expansions in
 # about 0.11 s (its receiver's backoff sleeps floor the wall time)
 REF_PF08184_T1_S, REF_PF08184_T1_NODES = 0.11, 60
@@ -315,6 +320,15 @@ def main():
         # PMC bytes over algorithmic bytes per launch (> 1: re-reads and
         # partial lines; the PMC read side is an upper bound, see the source)
         roof["traffic_ratio"] = traffic / alg_per_launch
+    gen = sum(r.generated for r, _ in results)
+    if kern_ms > 0 and gen and not results[-1][0].solo:
+        # the random-access view of the same kernel: every generated child
+        # probes its node-table slot (one random line read; at most one
+        # device-scope atomic), against the chip's measured random-load rate
+        rate = gen / (kern_ms / 1e3) / 1e9
+        roof["probes"] = {"achieved": rate, "peak": RANDOM_LOAD_PEAK_GS, "unit": "G probes/s",
+                          "frac": rate / RANDOM_LOAD_PEAK_GS, "atomic_peak": RANDOM_ATOMIC_PEAK_GS,
+                          "children_per_search": gen / args.steps, "source": "profiles/r2_atomic_rate.txt"}
     us_search = pmc.get("rocprof_expand_us_per_search_timed")
     if us_search:
         # the same algorithmic bytes per search over the expand time per
