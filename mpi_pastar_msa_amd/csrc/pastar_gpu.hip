@@ -1131,7 +1131,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     hc.n_shards = G;
     hc.kmax = cfg.kmax;
     hc.kmin = cfg.kmin;
-    hc.pool_chunks = pool_chunks_of(cfg);
+    hc.pool_chunks = c->pool.n / kChunk;  // the allocation (>= the request): stable across searches
     hc.maxch = maxch_of(cfg);
     hc.table_slots = c->nslots;
     hc.max_steps = cfg.max_steps;
@@ -1191,7 +1191,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.outbox = c->outbox.p;
     a.outbox_cap = cfg.outbox_cap;
     a.maxch = maxch_of(cfg);
-    a.pool_chunks = pool_chunks_of(cfg);
+    a.pool_chunks = c->pool.n / kChunk;
 
     const dim3 blk(kBlock);
     // about one resident wave of blocks: a block then walks several chunks
@@ -2273,7 +2273,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     hc.f0 = c->h0;
     hc.n_shards = 1;
     hc.kmax = hc.kmin = 1;
-    hc.pool_chunks = pool_chunks_of(cfg);
+    hc.pool_chunks = c->pool.n / kChunk;  // the allocation (>= the request): stable across searches
     hc.maxch = maxch_of(cfg);
     hc.table_slots = c->nslots;
     hc.cur_b = kBuckets;  // empty: appends lower it
@@ -2293,7 +2293,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     a.stats = c->stats.p;
     a.goal_g = c->goal.p;
     a.maxch = maxch_of(cfg);
-    a.pool_chunks = pool_chunks_of(cfg);
+    a.pool_chunks = c->pool.n / kChunk;
     c->lists_reopen = 0;
     c->lists_ready = true;
     return PASTAR_OK;
