@@ -92,7 +92,10 @@ typedef struct pastar_search_opts {
     int64_t batch_min;        /* a step with fewer nodes in its band also
                                  takes the next bands (up to 4); 0 = 1/8 of
                                  batch_nodes                               */
-    int64_t table_slots_log2; /* open+closed hash table capacity (log2)     */
+    int64_t table_slots_log2; /* open+closed hash table capacity (log2); 0 =
+                                 2^24 on a context's first search, then what
+                                 the last search needed at <= 25% load; an
+                                 explicit value is a floor under the latter */
     int64_t pool_entries;     /* open-list entry pool (all f buckets)       */
     int64_t subqueue_entries; /* entries one bucket sub-queue can hold      */
     int64_t max_steps;        /* safety stop (0 = unlimited)                */

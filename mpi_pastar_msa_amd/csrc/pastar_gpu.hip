@@ -1806,7 +1806,10 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     // (a repeated search of the same problem initialises only what it
     // needs), else 2^24 slots (512 MB, cleared in ~0.1 ms: kinase's first
     // search then runs without a capacity restart; tools/gpu/cold_probe.py)
-    cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : (c->learned_log2 > 0 ? c->learned_log2 : 24);
+    // (an explicit size is a floor: a repeated search never restarts below
+    // what the last one needed)
+    cfg.table_log2 = o.table_slots_log2 > 0 ? std::max((int)o.table_slots_log2, c->learned_log2)
+                                            : (c->learned_log2 > 0 ? c->learned_log2 : 24);
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
     // (the pool is never cleared: its size costs memory only, 2 GB here)
