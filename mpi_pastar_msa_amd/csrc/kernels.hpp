@@ -536,6 +536,14 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
+__device__ __forceinline__ unsigned wave_sum(unsigned v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o);
+    return v;
+}
+
 // Loads of words other blocks of the same launch update with atomics (the
 // fused select runs in the last expand block): coherent across XCDs.
 template <typename T>
@@ -673,7 +681,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 template <int KW, int PFS = 1, typename PP>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
-                                            int m, unsigned long long &claimed, unsigned long long &ovf,
+                                            int m, unsigned &claimed, unsigned &ovf,
                                             const LocalPush<KW> &lp, bool remote_in = false, bool has_pre = false,
                                             const SlotWords<KW, PFS> &pre = SlotWords<KW, PFS>{})
 {
@@ -1128,6 +1136,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     const int group = lane / lpn, glane = lane % lpn;
     const int leader_lane = group * lpn;
+    // one child round (2^N <= 64): this lane's child mask is glane for the
+    // whole launch, so its key increment is computed once
+    constexpr bool kOneRound = N > 0 && (1 << N) <= 64;
+    uint64_t kinc[KW];
+    {
+        const uint64_t zero[KW] = {};
+        child_key<N, KW>(P, n, zero, kOneRound ? glane : 0, kinc);
+    }
     __shared__ int2 terms_all[kWaves][terms_per_wave(N)];
     // batch offsets fit 32 bits (batch_nodes <= 2^30, checked on the host)
     __shared__ uint32_t prefix[kRanges + 1];
@@ -1160,7 +1176,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     StepStats *st = a.stats;
     const int w = view.band_log2, f0 = view.f0;
     const int bound = *(volatile int *)a.goal_g;
-    unsigned long long expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
+    // per-lane statistics of one launch (32-bit: at most a few million)
+    unsigned expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
     const int masks = 1 << n;
     __syncthreads();
     BPHASE(0)
@@ -1238,7 +1255,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                     // the table), so the wait counts do not depend on it
                     const int m = glane;
                     uint64_t ck[KW];
-                    child_key<N, KW>(P, n, par_.key, m, ck);
+                    if constexpr (kOneRound) {
+#pragma unroll
+                        for (int k = 0; k < KW; k++)
+                            ck[k] = par_.key[k] + kinc[k];
+                    } else {
+                        child_key<N, KW>(P, n, par_.key, m, ck);
+                    }
                     pf = slot_prefetch<KW, kPfSlots>(a.table, a.cap_mask, ck);
                     has_pf = m >= 1 && m < masks && !(m & par_.blocked);
                 }
@@ -1291,7 +1314,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                     valid = false;
             }
             if (valid) {
-                child_key<N, KW>(P, n, par_.key, m, ck);
+                if constexpr (kOneRound) {
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        ck[k] = par_.key[k] + kinc[k];
+                } else {
+                    child_key<N, KW>(P, n, par_.key, m, ck);
+                }
                 if (P.n_shards > 1) {
                     int cp[Parent<N, KW>::NMAX];
 #pragma unroll
@@ -1456,17 +1485,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     if (lane == 0) {
         unsigned long long *row = stat_row(st, blockIdx.x * kWaves + wave);
         if (expanded)
-            atomicAdd(&row[kStExpanded], expanded);
+            atomicAdd(&row[kStExpanded], (unsigned long long)expanded);
         if (reopen)
-            atomicAdd(&row[kStReopen], reopen);
+            atomicAdd(&row[kStReopen], (unsigned long long)reopen);
         if (generated)
-            atomicAdd(&row[kStGenerated], generated);
+            atomicAdd(&row[kStGenerated], (unsigned long long)generated);
         if (claimed)
-            atomicAdd(&row[kStClaimed], claimed);
+            atomicAdd(&row[kStClaimed], (unsigned long long)claimed);
         if (ovf)
-            atomicAdd(&row[kStOvfTable], ovf);
+            atomicAdd(&row[kStOvfTable], (unsigned long long)ovf);
         if (stale)
-            atomicAdd(&row[kStDropped], stale);
+            atomicAdd(&row[kStDropped], (unsigned long long)stale);
     }
 #ifdef PASTAR_PHASE_TIMERS
     if ((view.timing & 4) && timing && threadIdx.x == 0) {
@@ -1558,7 +1587,7 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     StepStats *st = a.stats;
     const int w = ctl->band_log2, f0 = ctl->f0;
     const int bound = *(volatile int *)a.goal_g;
-    unsigned long long claimed = 0, ovf = 0;
+    unsigned claimed = 0, ovf = 0;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
     const unsigned long long iters = (count + stride - 1) / stride;
     for (unsigned long long it = 0; it < iters; it++) {
@@ -1587,9 +1616,9 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     if (lane_id() == 0) {
         unsigned long long *row = stat_row(st, (blockIdx.x * blockDim.x + threadIdx.x) / 64);
         if (claimed)
-            atomicAdd(&row[kStClaimed], claimed);
+            atomicAdd(&row[kStClaimed], (unsigned long long)claimed);
         if (ovf)
-            atomicAdd(&row[kStOvfTable], ovf);
+            atomicAdd(&row[kStOvfTable], (unsigned long long)ovf);
     }
 }
 
