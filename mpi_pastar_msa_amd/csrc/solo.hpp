@@ -365,6 +365,32 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
             }
         }
     }
+    // two levels per pass (N <= 3, one parent): lane (group c, glane m)
+    // takes child c of the parent (group 0: child m) and, for c >= 1, that
+    // child's child m; the first move's constants per lane
+    constexpr bool TWO = ROUNDS == 1 && MASKS * MASKS <= 64;
+    const int c1 = group ? group : glane;
+    uint32_t kincA = 0;
+    int coffA[NP], gconstA = 0;
+    uint32_t bothA = 0;
+    {
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            kincA += ((c1 >> i) & 1u) << ksh[i];
+        int p = 0;
+#pragma unroll
+        for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+            for (int y = x + 1; y < N; y++, p++) {
+                const int bx = (c1 >> x) & 1, by = (c1 >> y) & 1;
+                coffA[p] = (bx ? prow[p] : 0) + by;
+                if (bx & by)
+                    bothA |= 1u << p;
+                else
+                    gconstA += (bx | by ? P.gap_open : P.gap_gap) * P.weight[p];
+            }
+        }
+    }
     const uint32_t goal_key = (uint32_t)P.goal_key[0] | 0x80000000u;
     const uint32_t origin_key = 0x80000000u;
     int h0 = 0;
@@ -522,6 +548,157 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
         }
         levels++;
         SOLO_PHASE_MARK(0);
+        if constexpr (TWO) {
+            if (nb == 1 && levels < a.max_levels) {
+                // one parent X: this level and the next in one pass.  The
+                // next level of the one-level pass would expand exactly X's
+                // improved children of this bucket (its whole batch, all
+                // current), so expanding them here is the same search.
+                SoloEntry be4;
+                if (hand) {
+                    const int L = __ffsll((long long)hand_bits) - 1;
+                    be4 = SoloEntry{__builtin_amdgcn_readlane(hand_key, L), __builtin_amdgcn_readlane(hand_slot, L),
+                                    __builtin_amdgcn_readlane(hand_g, L), __builtin_amdgcn_readlane(hand_f, L)};
+                } else {
+                    be4 = bat[cur * NBC];
+                }
+                const uint32_t xkey = (uint32_t)be4.x;
+                const int xslot = be4.y, xg = be4.z, xf = be4.w;
+                int posX[N], blockedX = 0;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    posX[i] = (int)((xkey >> ksh[i]) & (uint32_t)kbm[i]);
+                    blockedX |= (posX[i] >= len[i]) << i;
+                }
+                // child c1's position: blocked coordinates of its own moves
+                int blockedC = 0;
+#pragma unroll
+                for (int i = 0; i < N; i++)
+                    blockedC |= (posX[i] + ((c1 >> i) & 1) >= len[i]) << i;
+                int baseX[NP], baseC[NP];
+                {
+                    int p = 0;
+#pragma unroll
+                    for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+                        for (int y = x + 1; y < N; y++, p++) {
+                            baseX[p] = poff[p] + posX[x] * prow[p] + posX[y];
+                            baseC[p] = baseX[p] + coffA[p];
+                        }
+                    }
+                }
+                // X's node words and every lane's cells in one LDS round trip
+                const uint64_t pbest = best[xslot];
+                const int closedX = hcl[xslot].y;
+                int hvA[NP], cvX[NP], cvC[NP], hvB[NP];
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    hvA[p] = HCl[baseC[p]].x;
+                    cvX[p] = HCl[baseX[p]].y;
+                    cvC[p] = HCl[baseC[p]].y;
+                    hvB[p] = HCl[baseC[p] + coff[0][p]].x;
+                }
+                int dg1 = gconstA, h1 = 0, dg2 = gconst[0], h2 = 0;
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    h1 += hvA[p];
+                    dg1 += ((bothA >> p) & 1) ? cvX[p] : 0;
+                    h2 += hvB[p];
+                    dg2 += ((both[0] >> p) & 1) ? cvC[p] : 0;
+                }
+                const bool okX = (int)(pbest >> 32) == xg && xf < goal_g;
+                if (lane == 0) {
+                    if (okX) {
+                        reopen += closedX != kIntMax;
+                        hcl[xslot].y = xg;  // ClosedList[current.pos] (PAStar.cpp:351)
+                    }
+                    expanded += okX;
+                    dropped += !okX;
+                }
+                // level L: X's children on group 0
+                const bool v1 = okX && c1 >= 1 && !(c1 & blockedX);
+                const uint32_t ck1 = xkey + kincA;
+                const int g1 = xg + dg1, f1 = g1 + h1;
+                bool imp1 = false, cl1 = false;
+                int slot1 = 0;
+                if (group == 0 && v1) {
+                    slot1 = solo_relax(keys, best, hcl, lgC, ck1, g1, c1, xslot, h1, imp1, cl1);
+                    if (slot1 < 0)
+                        imp1 = false;
+                }
+                generated += group == 0 && v1;
+                claimed_n += (int)__popcll(__ballot(cl1));
+                if (__ballot(group == 0 && v1 && slot1 < 0))
+                    status = 2;
+                const bool goal1 = imp1 && ck1 == goal_key;
+                if (__ballot(goal1))
+                    goal_g = wave_min_i32(goal1 ? (g1 < goal_g ? g1 : goal_g) : goal_g);
+                const bool live1 = imp1 && f1 < goal_g;
+                const bool next1 = live1 && bucket(f1) <= bsel;
+                // children past the bucket: to the pile
+                const bool pile1 = live1 && !next1;
+                const uint64_t bp1 = __ballot(pile1);
+                if (pile1)
+                    pile[npile + __popcll(bp1 & below_me)] = solo_v2{slot1, f1};
+                npile += __popcll(bp1);
+                // level L + 1: group c expands child c (lane c of group 0)
+                const uint64_t nextbits = __ballot(group == 0 && next1);
+                const bool exp_c = group >= 1 && ((nextbits >> group) & 1ull);
+                const int slot_c = __shfl(slot1, group);
+                if (exp_c && glane == 0) {
+                    reopen += hcl[slot_c].y != kIntMax;
+                    hcl[slot_c].y = g1;
+                    expanded++;
+                }
+                const bool v2 = exp_c && glane >= 1 && !(glane & blockedC);
+                const uint32_t ck2 = ck1 + kinc[0];
+                const int g2 = g1 + dg2, f2 = g2 + h2;
+                bool imp2 = false, cl2 = false;
+                int slot2 = 0;
+                if (v2) {
+                    slot2 = solo_relax(keys, best, hcl, lgC, ck2, g2, glane, slot_c, h2, imp2, cl2);
+                    if (slot2 < 0)
+                        imp2 = false;
+                }
+                generated += v2;
+                claimed_n += (int)__popcll(__ballot(cl2));
+                if (__ballot(v2 && slot2 < 0))
+                    status = 2;
+                const bool goal2 = imp2 && ck2 == goal_key;
+                if (__ballot(goal2))
+                    goal_g = wave_min_i32(goal2 ? (g2 < goal_g ? g2 : goal_g) : goal_g);
+                const bool live2 = imp2 && f2 < goal_g;
+                const bool next2 = live2 && bucket(f2) <= bsel;
+                const uint64_t bn = __ballot(next2);
+                const int at = __popcll(bn & below_me);
+                const bool in_next = next2 && at < NBC;
+                SOLO_LDS SoloEntry *nxt2 = bat + (cur ^ 1) * NBC;
+                if (in_next)
+                    nxt2[at] = SoloEntry{(int)ck2, slot2, g2, f2};
+                const uint64_t nbits = __ballot(in_next);
+                const bool pile2 = live2 && !in_next;
+                const uint64_t bp2 = __ballot(pile2);
+                if (pile2)
+                    pile[npile + __popcll(bp2 & below_me)] = solo_v2{slot2, f2};
+                npile += __popcll(bp2);
+                if (npile + 64 > C || claimed_n > claim_limit)
+                    status = 2;
+                if (nextbits)
+                    levels++;  // the pass ran level L + 1 too
+                if (status)
+                    break;
+                cur ^= 1;
+                nb = __popcll(nbits);
+                hand = nb <= PPW;
+                hand_bits = nbits;
+                hand_key = (int)ck2;
+                hand_slot = slot2;
+                hand_g = g2;
+                hand_f = f2;
+                SOLO_PHASE_MARK(3);
+                continue;
+            }
+        }
         // expand the batch: PPW parents per pass, LPN lanes (child masks) each
         int nn = 0;
         SOLO_LDS SoloEntry *nxt = bat + (cur ^ 1) * NBC;
