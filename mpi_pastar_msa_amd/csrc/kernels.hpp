@@ -471,8 +471,9 @@ struct Ctl {
     unsigned long long body_ticks[12];  // profile: expand phases of block 0 (diagnostics)
     unsigned long long body_launches;
     // profile (PASTAR_PHASE_TIMERS builds): per-block chain statistics,
-    // {blocks, sum levels, max levels, sum rounds, max rounds, max ticks}
-    unsigned long long blk_stats[6];
+    // {blocks, sum levels, max levels, sum rounds, max rounds, max ticks},
+    // then continuation levels by parents: 1, 2..4, 5..16, more
+    unsigned long long blk_stats[10];
     int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step, pad1;
     unsigned long long dbg_w, dbg_r;
 };
@@ -1410,6 +1411,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         const int cnt = lq_count[cur] < lq_cap ? lq_count[cur] : lq_cap;  // read after the level's barrier
         if (cnt == 0)
             break;
+#ifdef PASTAR_PHASE_TIMERS
+        if ((view.timing & 4) && timing && threadIdx.x == 0)
+            atomicAdd(&ctl->blk_stats[cnt == 1 ? 6 : (cnt <= 4 ? 7 : (cnt <= 16 ? 8 : 9))], 1ull);
+#endif
         const int nxt = cur ^ 1;
         if (threadIdx.x == 0)
             lq_count[nxt] = 0;

@@ -1569,6 +1569,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::fprintf(stderr, "\n[pastar] blocks %llu over %llu launches: levels mean %.1f max %llu, rounds mean %.1f max %llu, "
                      "longest block %.2f us\n", h.blk_stats[0], h.body_launches, h.blk_stats[1] / nb, h.blk_stats[2],
                      h.blk_stats[3] / nb, h.blk_stats[4], h.blk_stats[5] * 1e-2);
+        std::fprintf(stderr, "[pastar] continuation levels by parents: 1: %llu, 2-4: %llu, 5-16: %llu, more: %llu\n",
+                     h.blk_stats[6], h.blk_stats[7], h.blk_stats[8], h.blk_stats[9]);
     }
     res->gap_ms = (double)h.gap_ticks * 1e-5;
     res->expand_launches = launches;
