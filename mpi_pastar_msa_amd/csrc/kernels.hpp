@@ -1145,6 +1145,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         const uint64_t zero[KW] = {};
         child_key<N, KW>(P, n, zero, kOneRound ? glane : 0, kinc);
     }
+    // two continuation levels per pass for a one-parent level (N = 4: the
+    // parent's 15 children and their 15 x 15 children on the block's 16
+    // groups); the key increment of this group's child mask
+    constexpr bool kTwoLevel = N == 4 && KW == 1;
+    uint64_t kinc_grp[KW];
+    {
+        const uint64_t zero[KW] = {};
+        child_key<N, KW>(P, n, zero, kTwoLevel ? wave * npw + group : 0, kinc_grp);
+    }
     __shared__ int2 terms_all[kWaves][terms_per_wave(N)];
     // batch offsets fit 32 bits (batch_nodes <= 2^30, checked on the host)
     __shared__ uint32_t prefix[kRanges + 1];
@@ -1419,6 +1428,136 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if (threadIdx.x == 0)
             lq_count[nxt] = 0;
         lds_barrier();
+        if constexpr (kTwoLevel) {
+            if (cnt == 1 && lvl + 1 < depth && P.n_shards == 1) {
+                // one parent: this level and the next in one pass.  The next
+                // level of the one-level pass would expand exactly this
+                // parent's improved children below f_limit (its whole queue);
+                // here group c expands child c right after group 0 relaxed it
+                // (without the one-level pass's re-read of the child's best:
+                // a child another block improved meanwhile is expanded at its
+                // older g, which only adds work the improvement then redoes)
+                __shared__ int kid_slot[16], kid_g[16];
+                __shared__ unsigned kid_exp;
+                const LEntry<KW> le = lq[cur][0];
+                const int c = wave * npw + group;  // 0: the parent, else its child c
+                const uint64_t *pslot = a.table + (uint64_t)le.slot * SW;
+                const uint64_t lbest = pslot[KW], laux = pslot[KW + 1];
+                Parent<N, KW> me;
+                int posX[N], blockedX = 0;
+                {
+                    const uint64_t pk[KW] = {le.key[0]};
+                    decode_key<N, KW>(P, n, pk, posX);
+                }
+#pragma unroll
+                for (int i = 0; i < N; i++)
+                    blockedX |= (posX[i] >= P.len[i]) << i;
+                me.key[0] = le.key[0] + kinc_grp[0];
+                me.blocked = 0;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    me.pos[i] = posX[i] + ((c >> i) & 1);
+                    me.blocked |= (me.pos[i] >= P.len[i]) << i;
+                }
+                me.pmask = c == 0 ? le.pmask : c;
+                me.g = le.g;
+                // this lane's target: group 0 lane m the parent's child m,
+                // group c lane m child c's child m
+                uint64_t tk[KW] = {me.key[0] + kinc[0]};
+                SlotWords<KW, kPfSlots> pf{};
+                auto prefetch = [&] { pf = slot_prefetch<KW, kPfSlots>(a.table, a.cap_mask, tk); };
+                stage_terms_fixed<N, KW>(P, pc, me, terms, glane, prefetch);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // the parent, as a one-level continuation entry
+                const bool okb = le.g + le.h < bound;
+                const bool okp = okb && (uint32_t)(lbest >> 32) >= (uint32_t)le.g;
+                if (threadIdx.x == 0) {
+                    if (okp) {
+                        reopen += (int)(uint32_t)laux != kIntMax;
+                        *(int *)(a.table + (uint64_t)le.slot * SW + KW + 1) = le.g;
+                        expanded++;
+                    }
+                    stale += okb && !okp;
+                }
+                // level L: the parent's children on group 0
+                const int m = glane;
+                const int2 d1 = child_cost<N>(Pg, npairs, terms, m);
+                const bool v1 = okp && c == 0 && m >= 1 && !(m & blockedX);
+                const int g1 = le.g + d1.x, h1 = d1.y, f1 = g1 + h1;
+                generated += v1;
+                bool imp1 = false, cl1 = false;
+                int64_t slot1 = 0;
+                if (v1 && f1 < bound) {
+                    slot1 = relax<KW, kPfSlots>(a.table, a.cap_mask, tk, g1, m, h1, imp1, cl1, true, pf);
+                    if (slot1 < 0) {
+                        ovf++;
+                        imp1 = false;
+                    }
+                    claimed += cl1;
+                    if (imp1 && tk[0] == P.goal_key[0])
+                        atomicMin(a.goal_g, g1);
+                }
+                const bool exp1 = imp1 && f1 < f_limit;
+                // improved children past the batch: the block's deferred
+                // open-list entries (route_child's out path)
+                {
+                    bool global = imp1 && !exp1;
+                    const Entry e1 = {(uint32_t)(slot1 < 0 ? 0 : slot1), f1};
+                    const uint64_t gm = __ballot(global);
+                    if (gm) {
+                        const int leader = __ffsll((long long)gm) - 1;
+                        int b0 = 0;
+                        if (lane == leader)
+                            b0 = atomicAdd(&out_n, __popcll(gm));
+                        b0 = bcast_lane(b0, leader);
+                        if (global) {
+                            const int pos = b0 + __popcll(gm & ((1ull << lane) - 1ull));
+                            if (pos < kOutCap) {
+                                outq[pos] = e1;
+                                global = false;
+                            }
+                        }
+                    }
+                    queue_append(a, global, bucket_of(f1, f0, w), e1, st, false);
+                }
+                if (c == 0) {
+                    kid_slot[m] = (int)slot1;
+                    kid_g[m] = g1;
+                }
+                const uint64_t eb = __ballot(c == 0 && exp1);
+                if (threadIdx.x == 0)
+                    kid_exp = (unsigned)eb;  // group 0 is lanes 0..15 of wave 0
+                lds_barrier();
+                // level L + 1: group c expands child c
+                const bool expc = c >= 1 && ((kid_exp >> c) & 1u);
+                const int gc = kid_g[c], slotc = kid_slot[c];
+                if (expc && glane == 0) {
+                    // the closing of the child (the one-level pass's store), as
+                    // a min: its old value tells a reopening
+                    const int old = atomicMin((int *)(a.table + (uint64_t)slotc * SW + KW + 1), gc);
+                    reopen += old != kIntMax;
+                    expanded++;
+                }
+                const int2 d2 = child_cost<N>(Pg, npairs, terms, m);
+                bool v2 = expc && m >= 1 && !(m & me.blocked);
+                const int g2 = gc + d2.x, h2 = d2.y;
+                if (v2) {
+                    generated++;
+                    if (g2 + h2 >= bound)
+                        v2 = false;
+                }
+                const LocalPush<KW> lq_next2{lvl + 2 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap,
+                                             outq, &out_n};
+                route_child<KW, kPfSlots>(a, P, st, f0, w, v2, true, P.shard, tk, g2, h2, m, claimed, ovf, lq_next2,
+                                          false, v2, pf);
+                BLK_COUNT(2, 1)
+                lds_barrier();
+                BPHASE(3)
+                cur = nxt;
+                lvl++;  // two levels
+                continue;
+            }
+        }
         const LocalPush<KW> lq_next{lvl + 1 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap, outq,
                                     &out_n};
         for (int base = 0; base < cnt; base += per_block) {
