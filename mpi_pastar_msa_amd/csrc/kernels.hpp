@@ -1126,8 +1126,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     const unsigned long long nb = view.n_batch;
     // blocks with work; with an empty batch block 0 still runs the tail
     // (the fused select of the first step)
+    // a batch of at most one entry per block (N = 4): each block takes one
+    // parent and starts its chain with the two-level pass below
+    const bool single = N == 4 && KW == 1 && nb > 0 && nb <= gridDim.x && P.n_shards == 1 && view.depth > 2;
+    const unsigned long long eff_per_block = single ? 1 : per_block;
     const unsigned long long nact =
-        nb ? ((nb + per_block - 1) / per_block < gridDim.x ? (nb + per_block - 1) / per_block : gridDim.x) : 1;
+        nb ? ((nb + eff_per_block - 1) / eff_per_block < gridDim.x ? (nb + eff_per_block - 1) / eff_per_block
+                                                                   : gridDim.x)
+           : 1;
     if (blockIdx.x >= nact)
         return;  // blocks beyond the batch leave at once
     const bool timing = (view.timing & 1) && nb;
@@ -1390,14 +1396,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // (entry: chunk table + pool, then the slot)
     const PSlot<KW> no_ps{};
     const uint32_t pf_lo = prefix[2 * lane], pf_hi = prefix[2 * lane + 1];
+    if (single) {
+        // the block's one batch entry, as a continuation entry of level 1
+        // (its current-ness re-checked there; the closing and the counts
+        // happen in the pass that expands it)
+        if (wave == 0) {
+            const unsigned long long node = blockIdx.x;
+            const int r = batch_range(pf_lo, pf_hi, node, 1, 64);
+            const Entry e = batch_entry_at(a, view, prefix, bstart, node, r);
+            const PSlot<KW> ps = load_pslot<KW>(a.table, e.slot);
+            if (lane == 0) {
+                const int g = (int)(ps.best >> 32), h = (int)(ps.aux >> 32);
+                if (g + h == e.f && e.f < bound) {
+                    LEntry<KW> le;
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        le.key[k] = ps.key[k];
+                    le.slot = e.slot;
+                    le.g = g;
+                    le.h = h;
+                    le.pmask = (int)(uint32_t)ps.best;
+                    lq[0][0] = le;
+                    lq_count[0] = 1;
+                } else {
+                    stale++;
+                }
+            }
+        }
+    }
     Entry e_nx{0, 0};
-    {
+    if (!single) {
         const unsigned long long node = (unsigned long long)blockIdx.x * per_block + wave * npw + group;
         const int r = batch_range(pf_lo, pf_hi, node, npw, lpn);
         if (node < nb)
             e_nx = batch_entry_at(a, view, prefix, bstart, node, r);
     }
-    for (unsigned long long chunk = blockIdx.x; chunk * per_block < nb; chunk += gridDim.x) {
+    for (unsigned long long chunk = blockIdx.x; !single && chunk * per_block < nb; chunk += gridDim.x) {
         const unsigned long long node = chunk * per_block + wave * npw + group;
         const bool ok = node < nb;
         const Entry e = e_nx;
