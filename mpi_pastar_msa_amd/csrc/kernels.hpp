@@ -1856,7 +1856,8 @@ __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restric
                                                             int *__restrict__ goal,
                                                             unsigned long long *__restrict__ census,
                                                             const uint32_t *__restrict__ stage,
-                                                            uint32_t *__restrict__ ctl_dst, int stage_words)
+                                                            uint32_t *__restrict__ ctl_dst, int stage_words,
+                                                            int seed_taken)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1877,10 +1878,14 @@ __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restric
             for (unsigned long long c = 0; c < used; c++)
                 row[c] = 0;
             q->W[b][sq] = 0;
-            q->R[b][sq] = 0;
+            // seed_taken: the origin, appended next at (bucket 0, sub-queue
+            // 0), is already the first batch the staged control block holds
+            q->R[b][sq] = seed_taken && b == 0 && sq == 0 ? 1 : 0;
         }
     }
     if (blockIdx.x == 0) {
+        if (seed_taken && !reset_queues && threadIdx.x == 0)
+            q->R[0][0] = 1;  // (the queues were cleared by a memset)
         for (int k = threadIdx.x; k < stage_words; k += blockDim.x)
             ctl_dst[k] = stage[k];
         unsigned long long *sw = reinterpret_cast<unsigned long long *>(stats);

@@ -970,7 +970,7 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
 // entries and cursors, the statistics, stamps, goal and census, and the
 // control block (+ origin record) from the pinned staging area c->h_stage,
 // `stage_bytes` of it (the host fills it before this call): one launch.
-int init_search(pastar_ctx *c, const SearchCfg &cfg, size_t stage_bytes)
+int init_search(pastar_ctx *c, const SearchCfg &cfg, size_t stage_bytes, bool seed_taken = false)
 {
     const int sw = slot_words_rt(c->kw);
     const unsigned long long maxch = maxch_of(cfg);
@@ -991,11 +991,11 @@ int init_search(pastar_ctx *c, const SearchCfg &cfg, size_t stage_bytes)
     if (sw == 4)
         hipLaunchKernelGGL((search_init_kernel<4>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
                            c->kw, c->queues.p, c->chunk_tab.p, maxch, reset_queues ? 1 : 0, c->stats.p, c->stamps.p,
-                           c->goal.p, c->census.p, stage, ctl_dst, words);
+                           c->goal.p, c->census.p, stage, ctl_dst, words, seed_taken ? 1 : 0);
     else
         hipLaunchKernelGGL((search_init_kernel<8>), dim3(blocks), dim3(kBlock), 0, c->stream, c->table.p, c->nslots,
                            c->kw, c->queues.p, c->chunk_tab.p, maxch, reset_queues ? 1 : 0, c->stats.p, c->stamps.p,
-                           c->goal.p, c->census.p, stage, ctl_dst, words);
+                           c->goal.p, c->census.p, stage, ctl_dst, words, seed_taken ? 1 : 0);
     PA_TRY(check_launch());
     return PASTAR_OK;
 }
@@ -1159,6 +1159,22 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
+    const bool seed_batch = c->tr == nullptr;
+    if (seed_batch) {
+        // one shard: the first batch is the origin alone, staged as select
+        // would cut it (bucket 0 = bucket(h0), sub-queue 0 of the one-block
+        // insert, position 0; the next kWide buckets included), so the first
+        // launch expands instead of only selecting
+        hc.n_batch = 1;
+        hc.batch_b = 0;
+        hc.batch_nb = kWide;
+        hc.cur_b = 0;
+        hc.has_work = 1;
+        hc.steps = 1;
+        hc.b_prefix[0] = 0;
+        for (int r = 1; r <= kRanges; r++)
+            hc.b_prefix[r] = 1;
+    }
     {
         const char *e = std::getenv("PASTAR_DEEP_BLOCKS");  // tuning override
         hc.deep_blocks = e && *e ? std::max(1, std::atoi(e)) : kDeepBlocks;
@@ -1216,7 +1232,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         int32_t tail[4] = {0, h0, (1 << c->n) - 1, 0};
         std::memcpy(rec.data() + 8 * KW, tail, 16);
         std::memcpy(c->h_stage + sizeof(Ctl), rec.data(), rb);
-        PA_TRY(init_search(c, cfg, sizeof(Ctl) + rb));
+        PA_TRY(init_search(c, cfg, sizeof(Ctl) + rb, seed_batch));
     }
     if (c->shard == origin_owner) {
         ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
