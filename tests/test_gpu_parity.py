@@ -197,6 +197,21 @@ def test_capacity_autogrow(kat):
             e2.pa_star(PAStarOpt(table_slots_log2=10, pool_entries=4096, autogrow=False))
 
 
+@pytest.mark.parametrize("depth,batch", [(1, 0), (2, 0), (3, 0), (128, 0), (128, 4), (128, 5000)])
+def test_continuation_variants_same_alignment(depth, batch, kat, oracles):
+    """N = 4 continuation paths: one level per launch (depth 1), one-level
+    continuation only (depth 2), the two-level pass (depth >= 3), batches
+    of one parent per block (small batch_nodes) or several: the same
+    optimal score and the reference's alignment."""
+    ref = kat["inputs"]["syn4x200_s1"]
+    with _engine("syn4x200_s1", kat) as e:
+        r = e.pa_star(PAStarOpt(depth=depth, batch_nodes=batch, mode="batched"))
+        assert r.score == ref["score"]
+        rows = e.alignment()
+        assert oracles["syn4x200_s1"].alignment_cost(rows) == ref["score"]
+        assert hashlib.md5("".join(x + "\n" for x in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
 def test_buffers_grow_only_across_searches(kat):
     """Search buffers are kept and only grow: a search sized below the last
     one runs in the front of the same table and pool (and its captured step

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/ev
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/ev/tests.log 2>&1 || { echo tests_fail; tail -30 gpurun_out/ev/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/ev/tests.log 2>&1 || { echo tests_fail; tail -30 gpurun_out/ev/tests.log; exit 1; }
 tail -2 gpurun_out/ev/tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ev/smoke.log 2>&1 || { echo smoke_fail; exit 1; }
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/ev/bench_syn4x200_s1.json 2> gpurun_out/ev/b1.err || { echo bench_fail; tail gpurun_out/ev/b1.err; exit 1; }
