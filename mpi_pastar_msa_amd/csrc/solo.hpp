@@ -16,10 +16,11 @@
 //      relaxation (g << 32 | parent mask, atomicMin: ties keep the smaller
 //      mask), staleness and closed rules; the search ends when no entry is
 //      left at or below the goal's bucket (check_stop, PAStar.cpp:480-547)
-//   3. the backtrace (backtrace.cpp:47-69) by lane 0, masks to HBM
+//   3. the backtrace (backtrace.cpp:47-69), masks to pinned host memory, then
+//      the result record and the completion word the host watches
 //   4. the node table dumped to HBM in the batched engine's slot layout (KW =
 //      1 keys; the solo probe rule, solo_lookup_kernel), for
-//      pastar_gpu_closed_lookup
+//      pastar_gpu_closed_lookup, after the result is published
 // Only the reference's equal gap costs (Cost.h:13) and coordinates that pack
 // into 31 bits take this path (keys and their hash are then 32-bit
 // arithmetic: the level loop is instruction-bound); the host falls back to
@@ -151,20 +152,28 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
         // min(63, bottom) steps: a band of few rows sweeps only that much
         // past the last column
         const int nsteps = L2 + 1 + (bottom < 63 ? bottom : 63);
+        // a chunk's costs are read one chunk ahead and its codes two ahead,
+        // so the sweep does not wait on the two dependent LDS reads; reads
+        // past the table only feed cells outside it (unclamped, as in
+        // pairalign_wave_kernel)
+        int nc[kPaChunk], code[kPaChunk];
+#pragma unroll
+        for (int u = 0; u < kPaChunk; u++)
+            nc[u] = crow[s2[j - u - 1]];
+#pragma unroll
+        for (int u = 0; u < kPaChunk; u++)
+            code[u] = s2[j - kPaChunk - u - 1];
         for (int t0 = 0; t0 < nsteps; t0 += kPaChunk) {
             const int j0 = j;
-            // unclamped (as in pairalign_wave_kernel): a column outside the
-            // table only feeds cells outside it; lb is lane 63's row below
-            // (+inf under the table), the old value of the DPP shift
-            int lb[kPaChunk], nc[kPaChunk];
+            // lb is lane 63's row below (+inf under the table), the old value
+            // of the DPP shift
+            int lb[kPaChunk], ncn[kPaChunk];
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++) {
                 lb[u] = band > 0 ? below[j0 - u].x : kPaInf;
-                nc[u] = s2[j0 - u - 1];
+                ncn[u] = crow[code[u]];
+                code[u] = s2[j0 - 2 * kPaChunk - u - 1];
             }
-#pragma unroll
-            for (int u = 0; u < kPaChunk; u++)
-                nc[u] = crow[nc[u]];
             solo_v2 cb[kPaChunk];
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++, j--) {
@@ -185,6 +194,9 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
                 if (row_ok && jj >= 0 && jj <= L2)
                     Trow[jj] = cb[u];
             }
+#pragma unroll
+            for (int u = 0; u < kPaChunk; u++)
+                nc[u] = ncn[u];
         }
         lds_fence();  // band k's top row lands before band k + 1 reads it
     }
@@ -823,40 +835,29 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     const int e_all = wave_sum_i32(expanded), r_all = wave_sum_i32(reopen);
     const int gen_all = wave_sum_i32(generated), d_all = wave_sum_i32(dropped);
 
-    // 3. backtrace from the goal along the parent slots (backtrace.cpp:47-69)
+    // 3. backtrace from the goal along the parent slots (backtrace.cpp:47-69):
+    // one dependent LDS read per step with the loop on scalars (every lane
+    // reads the same word); mask k waits in lane k % 64 and each 64 go to
+    // host memory in one store
     int path_len = 0, path_status = 0;
-    if (status == 1 && lane == 0) {
-        int slot = solo_lookup(keys, lgC, goal_key);
+    if (status == 1) {
+        int slot = __builtin_amdgcn_readfirstlane(solo_lookup(keys, lgC, goal_key));
         path_status = 2;
+        int mreg = 0;
         while (slot >= 0 && path_len < a.max_path) {
             if (slot == origin_slot) {
                 path_status = 1;
                 break;
             }
             const uint64_t b = best[slot];
-            a.masks[path_len++] = (int)((b >> 16) & 0xffff);
-            slot = (int)(b & 0xffff);
+            mreg = lane == (path_len & 63) ? (int)((b >> 16) & 0xffff) : mreg;
+            path_len++;
+            if ((path_len & 63) == 0)
+                a.masks[path_len - 64 + lane] = mreg;
+            slot = __builtin_amdgcn_readfirstlane((int)(b & 0xffff));
         }
-    }
-    // 4. the node table to HBM (kernels.hpp slot layout: key word with bit 63
-    // set, g << 32 | mask, closed | h << 32; the solo probe order)
-    if (status == 1) {
-        ulonglong2 *d = reinterpret_cast<ulonglong2 *>(a.dump);
-        for (int k0 = 0; k0 < C; k0 += 256) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = k0 + u * 64 + lane;
-                if (k < C) {
-                    const uint32_t key = keys[k];
-                    const uint64_t b = best[k];
-                    const solo_v2 v = hcl[k];
-                    const uint64_t k64 = key ? (kMark | (key & 0x7fffffffu)) : 0;
-                    const uint64_t bm = b == ~0ull ? b : ((b & 0xffffffff00000000ull) | ((b >> 16) & 0xffff));
-                    d[2 * k] = make_ulonglong2(k64, bm);
-                    d[2 * k + 1] = make_ulonglong2((uint64_t)(uint32_t)v.y | ((uint64_t)(uint32_t)v.x << 32), 0ull);
-                }
-            }
-        }
+        if (lane < (path_len & 63))
+            a.masks[(path_len & ~63) + lane] = mreg;
     }
     if (lane == 0) {
         SoloOut o;
@@ -891,6 +892,28 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
         // result and the path are in host memory before it (system fence)
         __threadfence_system();
         __hip_atomic_store(a.done, a.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // 4. the node table to HBM (kernels.hpp slot layout: key word with bit 63
+    // set, g << 32 | mask, closed | h << 32; the solo probe order), after the
+    // result is published: the host has its answer while this runs, and
+    // pastar_gpu_closed_lookup's kernel is stream-ordered after this one
+    if (status == 1) {
+        ulonglong2 *d = reinterpret_cast<ulonglong2 *>(a.dump);
+        for (int k0 = 0; k0 < C; k0 += 256) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = k0 + u * 64 + lane;
+                if (k < C) {
+                    const uint32_t key = keys[k];
+                    const uint64_t b = best[k];
+                    const solo_v2 v = hcl[k];
+                    const uint64_t k64 = key ? (kMark | (key & 0x7fffffffu)) : 0;
+                    const uint64_t bm = b == ~0ull ? b : ((b & 0xffffffff00000000ull) | ((b >> 16) & 0xffff));
+                    d[2 * k] = make_ulonglong2(k64, bm);
+                    d[2 * k + 1] = make_ulonglong2((uint64_t)(uint32_t)v.y | ((uint64_t)(uint32_t)v.x << 32), 0ull);
+                }
+            }
+        }
     }
 }
 

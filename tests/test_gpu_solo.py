@@ -151,3 +151,30 @@ def test_solo_pair_tables_and_h_after_search(kat):
         assert e.initial_node().f == ref["h_origin"]
         for k in range(e.npairs):
             np.testing.assert_array_equal(e.pair_table(k), o.pair_table(k))
+
+
+@pytest.mark.parametrize("length,mutate", [(64, False), (100, False), (100, True)])
+def test_solo_long_paths(length, mutate):
+    """Backtraces of 64 and more steps (the path's masks leave the kernel 64
+    at a time): two sequences whose alignment has at least `length` columns,
+    identical (a diagonal path of exactly `length` steps) or mutated."""
+    rng = random.Random(length)
+    aa = "ACDEFGHIKLMNPQRSTVWY"
+    a = "".join(rng.choice(aa) for _ in range(length))
+    b = a
+    if mutate:
+        b = "".join(rng.choice(aa) if rng.random() < 0.2 else ch for ch in a if rng.random() > 0.1)
+    seqs = [a, b]
+    o = orc.Oracle(seqs=seqs)
+    ref = o.astar()
+    with Engine(seqs).init() as e:
+        r = e.pa_star(PAStarOpt(mode="solo"))
+        assert r.solo == 1 and r.score == ref["score"]
+        rows = e.alignment()
+        assert [row.replace("-", "") for row in rows] == seqs
+        assert o.alignment_cost(rows) == ref["score"]
+        assert len(rows[0]) >= length
+        if not mutate:
+            assert rows == seqs
+        rb = e.pa_star(PAStarOpt(mode="batched"))
+        assert rb.score == r.score and e.alignment() == rows
