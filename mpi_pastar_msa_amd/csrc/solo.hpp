@@ -233,25 +233,37 @@ __device__ __forceinline__ int solo_relax(SOLO_LDS uint32_t *keys, SOLO_LDS uint
 {
     const uint32_t cmask = (1u << cap_log2) - 1u;
     uint32_t idx = solo_hash(key, cap_log2);
-    for (uint32_t probe = 0; probe <= cmask; probe++) {
-        uint32_t prev = 0;
-        __hip_atomic_compare_exchange_strong(&keys[idx], &prev, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint64_t seen = best[idx];  // after this instruction's claims (in-order LDS)
-        if (prev == 0 || prev == key) {
-            claimed = prev == 0;
-            if (claimed)
-                hcl[idx].x = h;
-            const uint64_t nb = solo_best(g, mask, pslot);
-            improved = nb < seen && (uint32_t)(seen >> 32) > (uint32_t)g;
-            if (nb < seen)
-                __hip_atomic_fetch_min(&best[idx], nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return (int)idx;
+    // the first probe straight-line (the table stays at most 3/4 full, most
+    // relaxes settle here); only a wave with a lane on an occupied slot
+    // enters the probing loop, so the common path carries no loop-exit mask
+    // bookkeeping
+    uint32_t prev = 0;
+    __hip_atomic_compare_exchange_strong(&keys[idx], &prev, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint64_t seen = best[idx];  // after this instruction's claims (in-order LDS)
+    bool hit = prev == 0 || prev == key;
+    if (__builtin_expect(__ballot(!hit) != 0ull, 0)) {
+        for (uint32_t probe = 1; !hit && probe <= cmask; probe++) {
+            idx = (idx + 1) & cmask;
+            prev = 0;
+            __hip_atomic_compare_exchange_strong(&keys[idx], &prev, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            seen = best[idx];
+            hit = prev == 0 || prev == key;
         }
-        idx = (idx + 1) & cmask;
+        if (!hit) {
+            improved = claimed = false;
+            return -1;
+        }
     }
-    improved = claimed = false;
-    return -1;
+    // unconditional stores (no exec-mask branches): h is the key's own, so
+    // rewriting it is harmless, and a min that does not lower is a no-op
+    claimed = prev == 0;
+    hcl[idx].x = h;
+    const uint64_t nb = solo_best(g, mask, pslot);
+    improved = nb < seen && (uint32_t)(seen >> 32) > (uint32_t)g;
+    __hip_atomic_fetch_min(&best[idx], nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (int)idx;
 }
 
 __device__ __forceinline__ int solo_lookup(const SOLO_LDS uint32_t *keys, int cap_log2, uint32_t key)
