@@ -232,6 +232,9 @@ class Engine:
         self.npairs = npairs
         self.pairs = [(x, y) for x in range(self.n - 1) for y in range(x + 1, self.n)]
         self._ready = False
+        self._result = nat.pastar_result()
+        self._so, self._so_key = None, None
+        self._rows_buf = None
 
     def close(self):
         if self._ctx:
@@ -337,10 +340,13 @@ class Engine:
             raise ValueError("Invalid number of threads")
         if not self._ready:
             self.init()
-        r = nat.pastar_result()
-        so = opt.search_opts()
-        check(lib().pastar_gpu_search(self._ctx, ctypes.byref(so), ctypes.byref(r)))
-        return SearchResult(**r.as_dict())
+        r = self._result
+        # the options struct is rebuilt only when an option changed
+        key = tuple(opt.__dict__.values())
+        if key != self._so_key:
+            self._so, self._so_key = opt.search_opts(), key
+        check(lib().pastar_gpu_search(self._ctx, ctypes.byref(self._so), ctypes.byref(r)))
+        return SearchResult(*r.as_tuple())
 
     def closed_lookup(self, coord):
         c = (ctypes.c_uint16 * MAX_SEQ)(*coord)
@@ -353,12 +359,13 @@ class Engine:
 
     def alignment(self):
         """Backtrace rows (collective over shards)."""
-        stride = sum(len(s) for s in self.sequences.seqs) + 1
-        buf = ctypes.create_string_buffer(self.n * stride)
-        cols = ctypes.c_int()
+        if self._rows_buf is None:  # one buffer per engine, reused
+            stride = sum(len(s) for s in self.sequences.seqs) + 1
+            self._rows_buf = (ctypes.create_string_buffer(self.n * stride), stride, ctypes.c_int())
+        buf, stride, cols = self._rows_buf
         check(lib().pastar_gpu_alignment(self._ctx, buf, stride, ctypes.byref(cols)))
-        raw = buf.raw
-        return [raw[i * stride:i * stride + cols.value].decode("latin-1") for i in range(self.n)]
+        raw, n = buf.raw, cols.value
+        return [raw[i * stride:i * stride + n].decode("latin-1") for i in range(self.n)]
 
 
 def _c_nodes(nodes):
