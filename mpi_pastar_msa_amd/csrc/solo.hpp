@@ -121,7 +121,7 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // wave; lane 63 of band k reads the row below from band k - 1's top row in T.
 __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int p, SOLO_LDS solo_v2 *HCl,
                                                const SOLO_LDS int *sub, const SOLO_LDS uint8_t *codes,
-                                               SOLO_LDS int *subw)
+                                               SOLO_LDS int *subw, SOLO_LDS solo_v2 *sink)
 {
     const int lane = lane_id();
     const int x = P.pair_x[p], y = P.pair_y[p], wgt = P.weight[p];
@@ -188,11 +188,13 @@ __device__ __forceinline__ void solo_pairalign(const SOLO_LDS DevProblem &P, int
                 cb[u] = solo_v2{mm, cost_here};
                 m = j <= L2 ? mm : m;  // only the columns right of the table stay +inf
             }
+            // cells outside the table go to this lane's sink word: every
+            // store is unconditional (no exec-mask branches)
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++) {
                 const int jj = j0 - u;
-                if (row_ok && jj >= 0 && jj <= L2)
-                    Trow[jj] = cb[u];
+                SOLO_LDS solo_v2 *dst = row_ok && (unsigned)jj <= (unsigned)L2 ? Trow + jj : sink + lane;
+                *dst = cb[u];
             }
 #pragma unroll
             for (int u = 0; u < kPaChunk; u++)
@@ -336,8 +338,11 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
 
     // 1. PairAlign, pair p on wave p % 4
     SOLO_LDS int *subw = lds_at<int>(smem, a.off_subw) + wave * (a.alpha2 + 1);
+    // the sinks of the cells outside a table: 64 words per wave in the pile,
+    // unused until the search (C >= 256 slots of 8 B)
+    static_assert((1 << kSoloMinCapLog2) >= kSoloThreads, "a pile word per PairAlign lane");
     for (int p = wave; p < NP; p += kSoloThreads / 64)
-        solo_pairalign(P, p, HCl, sub, codes, subw);
+        solo_pairalign(P, p, HCl, sub, codes, subw, pile + wave * 64);
     __syncthreads();
     if (wave != 0)
         return;
@@ -856,17 +861,27 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
         int slot = __builtin_amdgcn_readfirstlane(solo_lookup(keys, lgC, goal_key));
         path_status = 2;
         int mreg = 0;
-        while (slot >= 0 && path_len < a.max_path) {
-            if (slot == origin_slot) {
-                path_status = 1;
-                break;
+        if (slot == origin_slot)
+            path_status = 1;
+        if (slot >= 0 && slot != origin_slot) {
+            // pipelined: the parent's word is requested as soon as its slot
+            // is known, ahead of this step's mask bookkeeping (the read of
+            // the origin's parent, slot 0xffff masked into the table, is
+            // issued and dropped)
+            uint64_t b = best[slot];
+            while (path_len < a.max_path) {
+                const int nxt = __builtin_amdgcn_readfirstlane((int)(b & 0xffff));
+                const uint64_t bn = best[nxt & (C - 1)];
+                mreg = lane == (path_len & 63) ? (int)((b >> 16) & 0xffff) : mreg;
+                path_len++;
+                if ((path_len & 63) == 0)
+                    a.masks[path_len - 64 + lane] = mreg;
+                if (nxt == origin_slot) {
+                    path_status = 1;
+                    break;
+                }
+                b = bn;
             }
-            const uint64_t b = best[slot];
-            mreg = lane == (path_len & 63) ? (int)((b >> 16) & 0xffff) : mreg;
-            path_len++;
-            if ((path_len & 63) == 0)
-                a.masks[path_len - 64 + lane] = mreg;
-            slot = __builtin_amdgcn_readfirstlane((int)(b & 0xffff));
         }
         if (lane < (path_len & 63))
             a.masks[(path_len & ~63) + lane] = mreg;
