@@ -283,6 +283,49 @@ __device__ __forceinline__ int solo_lookup(const SOLO_LDS uint32_t *keys, int ca
     return -1;
 }
 
+// The backtrace by pointer jumping (backtrace.cpp:47-69 follows the parent
+// chain one node at a time): level j of `anc` holds every slot's 2^j-th
+// ancestor, built by all four waves from the parent slots in the best words
+// (the origin, empty slots and broken links point to themselves).  Eight
+// levels of C 16-bit slots take the pile and batch areas (16 B per slot),
+// free once the search is over.  Every wave of the block must call it.
+constexpr int kLiftLevels = 8;
+
+__device__ __forceinline__ void solo_lift_levels(const SOLO_LDS uint32_t *keys, const SOLO_LDS uint64_t *best,
+                                                 SOLO_LDS uint16_t *anc, int C, int origin_slot)
+{
+    for (int s = threadIdx.x; s < C; s += kSoloThreads) {
+        const int p = (int)(best[s] & 0xffff);
+        anc[s] = (uint16_t)(keys[s] == 0 || s == origin_slot || p >= C ? s : p);
+    }
+    __syncthreads();
+    for (int j = 1; j < kLiftLevels; j++) {
+        const SOLO_LDS uint16_t *prev = anc + (j - 1) * C;
+        SOLO_LDS uint16_t *cur = anc + j * C;
+        for (int s = threadIdx.x; s < C; s += kSoloThreads)
+            cur[s] = prev[prev[s]];
+        __syncthreads();
+    }
+}
+
+// The node table to HBM (kernels.hpp slot layout: key word with bit 63 set,
+// g << 32 | mask, closed | h << 32; the solo probe order), by threads
+// first, first + stride, ...
+__device__ __forceinline__ void solo_dump(const SOLO_LDS uint32_t *keys, const SOLO_LDS uint64_t *best,
+                                          const SOLO_LDS solo_v2 *hcl, int C, uint64_t *dump, int first, int stride)
+{
+    ulonglong2 *d = reinterpret_cast<ulonglong2 *>(dump);
+    for (int k = first; k < C; k += stride) {
+        const uint32_t key = keys[k];
+        const uint64_t b = best[k];
+        const solo_v2 v = hcl[k];
+        const uint64_t k64 = key ? (kMark | (key & 0x7fffffffu)) : 0;
+        const uint64_t bm = b == ~0ull ? b : ((b & 0xffffffff00000000ull) | ((b >> 16) & 0xffff));
+        d[2 * k] = make_ulonglong2(k64, bm);
+        d[2 * k + 1] = make_ulonglong2((uint64_t)(uint32_t)v.y | ((uint64_t)(uint32_t)v.x << 32), 0ull);
+    }
+}
+
 // A batch entry carries the parent as queued, {key, slot, g, f}, so a level
 // reads its parents in one 16-B LDS load and their pair cells in the next
 // round trip.  A pile entry is {slot, f}.
@@ -344,8 +387,23 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     for (int p = wave; p < NP; p += kSoloThreads / 64)
         solo_pairalign(P, p, HCl, sub, codes, subw, pile + wave * 64);
     __syncthreads();
-    if (wave != 0)
+    // what waves 1..3 need from the search: its status, whether the
+    // backtrace lifts, and then they dump the node table (4.)
+    // (in the distance tables' staging area, free after PairAlign; no
+    // static LDS beside the dynamic 160 KB).  Every branch around a block
+    // barrier is on a scalar (readfirstlane): a branch the compiler took
+    // for divergent would run the other side's s_barrier with exec = 0
+    SOLO_LDS int *shv = lds_at<int>(smem, a.off_subw);  // [0] status, [1] lift
+    SOLO_LDS uint16_t *anc = (SOLO_LDS uint16_t *)pile;  // the backtrace's ancestor levels
+    const int origin_slot = (int)solo_hash(0x80000000u, lgC);
+    if (__builtin_amdgcn_readfirstlane(wave) != 0) {
+        __syncthreads();  // wave 0's search
+        if (__builtin_amdgcn_readfirstlane(shv[1]))
+            solo_lift_levels(keys, best, anc, C, origin_slot);
+        if (__builtin_amdgcn_readfirstlane(shv[0]) == 1)
+            solo_dump(keys, best, hcl, C, a.dump, tid - 64, kSoloThreads - 64);
         return;
+    }
     const unsigned long long t_tables = device_clock();
 
     // 2. the search, wave 0 alone (no block barriers: a wave's LDS accesses
@@ -494,7 +552,6 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     };
 
     // seed the origin (Sequences::get_initial_node, Sequences.cpp:70-77)
-    const int origin_slot = (int)solo_hash(origin_key, lgC);
     if (lane == 0) {
         keys[origin_slot] = origin_key;
         best[origin_slot] = solo_best(0, MASKS - 1, 0xffff);
@@ -852,36 +909,83 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     const int e_all = wave_sum_i32(expanded), r_all = wave_sum_i32(reopen);
     const int gen_all = wave_sum_i32(generated), d_all = wave_sum_i32(dropped);
 
-    // 3. backtrace from the goal along the parent slots (backtrace.cpp:47-69):
-    // one dependent LDS read per step with the loop on scalars (every lane
-    // reads the same word); mask k waits in lane k % 64 and each 64 go to
-    // host memory in one store
+    // 3. the backtrace (backtrace.cpp:47-69), by pointer jumping or by the
+    // walk.  Lifted: the goal's distance D to the origin by jumps of 2^j
+    // (greedy from the top level: a jump is taken while it stays short of
+    // the origin), then lane k finds the goal's k-th ancestor from the bits
+    // of k, and its mask is the path's k-th
+    int goal_slot = -1;
+    if (status == 1)
+        goal_slot = __builtin_amdgcn_readfirstlane(solo_lookup(keys, lgC, goal_key));
+    // the lift costs ~8 levels x C / 256 slot updates per thread, the walk
+    // ~85 ns per step (at least the longest sequence's length): the lift
+    // when the path is surely longer than C / 32 steps (PF08184: 59 against
+    // 32 at 1024 slots, tail 5.6 -> 3.6 us), else the walk
+    int maxlen = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        maxlen = len[i] > maxlen ? len[i] : maxlen;
+    const bool found = status == 1 && goal_slot >= 0 && goal_slot != origin_slot;
+    const bool lift = __builtin_amdgcn_readfirstlane(found && maxlen * 32 > C);
+    if (lane == 0) {
+        shv[0] = status;
+        shv[1] = lift ? 1 : 0;
+    }
+    __syncthreads();
     int path_len = 0, path_status = 0;
-    if (status == 1) {
-        int slot = __builtin_amdgcn_readfirstlane(solo_lookup(keys, lgC, goal_key));
-        path_status = 2;
-        int mreg = 0;
-        if (slot == origin_slot)
-            path_status = 1;
-        if (slot >= 0 && slot != origin_slot) {
-            // pipelined: the parent's word is requested as soon as its slot
-            // is known, ahead of this step's mask bookkeeping (the read of
-            // the origin's parent, slot 0xffff masked into the table, is
-            // issued and dropped)
-            uint64_t b = best[slot];
-            while (path_len < a.max_path) {
-                const int nxt = __builtin_amdgcn_readfirstlane((int)(b & 0xffff));
-                const uint64_t bn = best[nxt & (C - 1)];
-                mreg = lane == (path_len & 63) ? (int)((b >> 16) & 0xffff) : mreg;
-                path_len++;
-                if ((path_len & 63) == 0)
-                    a.masks[path_len - 64 + lane] = mreg;
-                if (nxt == origin_slot) {
-                    path_status = 1;
-                    break;
-                }
-                b = bn;
+    if (status == 1)
+        path_status = goal_slot == origin_slot ? 1 : 2;
+    if (lift) {
+        solo_lift_levels(keys, best, anc, C, origin_slot);
+        constexpr int kTop = 1 << (kLiftLevels - 1);
+        const SOLO_LDS uint16_t *top = anc + (kLiftLevels - 1) * C;
+        int x = goal_slot, D = 0;
+        while (top[x] != origin_slot && D < a.max_path) {
+            x = top[x];
+            D += kTop;
+        }
+        for (int j = kLiftLevels - 2; j >= 0; j--) {
+            const int y = anc[j * C + x];
+            if (y != origin_slot) {
+                x = y;
+                D += 1 << j;
             }
+        }
+        D = __builtin_amdgcn_readfirstlane(D + 1);  // x is now one step from the origin
+        if (anc[x] == origin_slot && D <= a.max_path) {
+            path_status = 1;
+            path_len = D;
+            for (int k = lane; k < D; k += 64) {
+                int y = goal_slot, r = k;
+                for (; r >= kTop; r -= kTop)
+                    y = top[y];
+#pragma unroll
+                for (int j = 0; j < kLiftLevels - 1; j++)
+                    if ((r >> j) & 1)
+                        y = anc[j * C + y];
+                a.masks[k] = (int)((best[y] >> 16) & 0xffff);
+            }
+        }
+    } else if (found) {
+        // the walk on scalars: every lane reads the same parent word, the
+        // next one is requested before the step's bookkeeping (the read of
+        // the origin's parent, slot 0xffff masked into the table, is issued
+        // and dropped), and mask k waits in lane k % 64 until 64 of them go
+        // to host memory in one store
+        int slot = goal_slot, mreg = 0;
+        uint64_t b = best[slot];
+        while (path_len < a.max_path) {
+            const int nxt = __builtin_amdgcn_readfirstlane((int)(b & 0xffff));
+            const uint64_t bn = best[nxt & (C - 1)];
+            mreg = lane == (path_len & 63) ? (int)((b >> 16) & 0xffff) : mreg;
+            path_len++;
+            if ((path_len & 63) == 0)
+                a.masks[path_len - 64 + lane] = mreg;
+            if (nxt == origin_slot) {
+                path_status = 1;
+                break;
+            }
+            b = bn;
         }
         if (lane < (path_len & 63))
             a.masks[(path_len & ~63) + lane] = mreg;
@@ -920,28 +1024,9 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
         __threadfence_system();
         __hip_atomic_store(a.done, a.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // 4. the node table to HBM (kernels.hpp slot layout: key word with bit 63
-    // set, g << 32 | mask, closed | h << 32; the solo probe order), after the
-    // result is published: the host has its answer while this runs, and
+    // 4. the node table dump runs on waves 1..3 (solo_dump), beside the
+    // result's publication: the host has its answer meanwhile, and
     // pastar_gpu_closed_lookup's kernel is stream-ordered after this one
-    if (status == 1) {
-        ulonglong2 *d = reinterpret_cast<ulonglong2 *>(a.dump);
-        for (int k0 = 0; k0 < C; k0 += 256) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = k0 + u * 64 + lane;
-                if (k < C) {
-                    const uint32_t key = keys[k];
-                    const uint64_t b = best[k];
-                    const solo_v2 v = hcl[k];
-                    const uint64_t k64 = key ? (kMark | (key & 0x7fffffffu)) : 0;
-                    const uint64_t bm = b == ~0ull ? b : ((b & 0xffffffff00000000ull) | ((b >> 16) & 0xffff));
-                    d[2 * k] = make_ulonglong2(k64, bm);
-                    d[2 * k + 1] = make_ulonglong2((uint64_t)(uint32_t)v.y | ((uint64_t)(uint32_t)v.x << 32), 0ull);
-                }
-            }
-        }
-    }
 }
 
 // Closed-list lookup in a solo search's dumped node table (kernels.hpp

@@ -153,16 +153,21 @@ def test_solo_pair_tables_and_h_after_search(kat):
             np.testing.assert_array_equal(e.pair_table(k), o.pair_table(k))
 
 
-@pytest.mark.parametrize("length,mutate", [(64, False), (100, False), (100, True)])
+@pytest.mark.parametrize("length,mutate", [(64, False), (100, False), (100, True), (100, "insert")])
 def test_solo_long_paths(length, mutate):
-    """Backtraces of 64 and more steps (the path's masks leave the kernel 64
-    at a time): two sequences whose alignment has at least `length` columns,
-    identical (a diagonal path of exactly `length` steps) or mutated."""
+    """Backtraces of 64 and more steps, by the walk (masks leave the kernel 64
+    at a time) or by pointer jumping (a path longer than 128 steps takes a
+    whole top-level jump): two sequences whose alignment has at least
+    `length` columns, identical (a diagonal path of exactly `length` steps),
+    mutated, or the second with ~30 insertions (a path of >= 129 steps)."""
     rng = random.Random(length)
     aa = "ACDEFGHIKLMNPQRSTVWY"
     a = "".join(rng.choice(aa) for _ in range(length))
     b = a
-    if mutate:
+    if mutate == "insert":
+        b = "".join(ch + (rng.choice(aa) if rng.random() < 0.3 else "") for ch in a)
+        assert len(b) >= 129
+    elif mutate:
         b = "".join(rng.choice(aa) if rng.random() < 0.2 else ch for ch in a if rng.random() > 0.1)
     seqs = [a, b]
     o = orc.Oracle(seqs=seqs)
