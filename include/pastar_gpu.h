@@ -280,6 +280,23 @@ int pastar_gpu_lists_erase(pastar_ctx *ctx, const uint16_t *pos, int which, int 
 /* Reopenings since pastar_gpu_lists_reset (nodes_reopen, PAStar.cpp:232). */
 int pastar_gpu_lists_reopened(pastar_ctx *ctx, int64_t *reopened);
 
+/* ---- MPI-compatible wire frame -------------------------
+ * The reference's inter-rank message frame, byte-identical to what its
+ * pastar_lz4_en emits (lz4sup.cpp:13-43): u32 total, u32 LZ4 bound, u32
+ * payload + 1, then the LZ4 block of the payload and a trailing NUL.  Host
+ * code, no device needed; the record exchange of this engine stays on RCCL.
+ *   pastar_lz4_en (lz4sup.cpp:13)   pastar_wire_frame_bound + _encode
+ *   pastar_lz4_dec (lz4sup.cpp:45)  pastar_wire_frame_decode: writes the
+ *                                   payload and its NUL (*out_len = len + 1)
+ *   Node<N>::serialize (Node.h:57-64) field order, packed little-endian
+ *   (12 + 2N bytes a node: g, f, pos[N], parenti)
+ *                                   pastar_wire_pack_nodes / _unpack_nodes */
+int pastar_wire_frame_bound(int64_t len, int64_t *bound);
+int pastar_wire_frame_encode(const void *payload, int64_t len, void *out, int64_t cap, int64_t *out_len);
+int pastar_wire_frame_decode(const void *frame, int64_t frame_len, void *out, int64_t cap, int64_t *out_len);
+int pastar_wire_pack_nodes(const pastar_node *nodes, int count, int n, void *out, int64_t cap, int64_t *out_len);
+int pastar_wire_unpack_nodes(const void *in, int64_t len, int n, pastar_node *out, int cap, int *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -149,6 +149,16 @@ SIGNATURES = {
     "pastar_gpu_lists_erase": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16), ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int)]),
     "pastar_gpu_lists_reopened": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    # MPI-compatible wire frame (host only)
+    "pastar_wire_frame_bound": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_wire_frame_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_wire_frame_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                                ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_wire_pack_nodes": (ctypes.c_int, [ctypes.POINTER(pastar_node), ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_wire_unpack_nodes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.POINTER(pastar_node), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
 }
 
 _lib = None

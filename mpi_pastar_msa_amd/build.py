@@ -26,7 +26,7 @@ COMMON = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=
 # phase timers of the expand kernel, read with PASTAR_TIMING_MASK=5)
 COMMON += os.environ.get("PASTAR_HIPCC_FLAGS", "").split()
 
-LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp"]
+LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp", "wire.cpp"]
 LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp", "solo.hpp", "lists.hpp"]
 
 

@@ -377,6 +377,52 @@ def _c_nodes(nodes):
     return arr
 
 
+def lz4_en(payload):
+    """pastar_lz4_en (lz4sup.cpp:13-43): the reference's wire frame of
+    `payload` (bytes), byte-identical to the reference's; the trailing NUL
+    of the reference's std::string is compressed with it."""
+    payload = bytes(payload)
+    bound = ctypes.c_int64()
+    check(lib().pastar_wire_frame_bound(len(payload), ctypes.byref(bound)))
+    out = ctypes.create_string_buffer(bound.value)
+    n = ctypes.c_int64()
+    check(lib().pastar_wire_frame_encode(payload, len(payload), out, bound.value, ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
+def lz4_dec(frame):
+    """pastar_lz4_dec (lz4sup.cpp:45-70): the frame's decoded bytes, the
+    trailing NUL included (the reference returns that length too)."""
+    frame = bytes(frame)
+    if len(frame) < 12:
+        raise nat.NativeError(-1, "frame shorter than its header")  # PASTAR_EINVAL
+    orig = int.from_bytes(frame[8:12], "little")
+    out = ctypes.create_string_buffer(max(orig, 1))
+    n = ctypes.c_int64()
+    check(lib().pastar_wire_frame_decode(frame, len(frame), out, orig, ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
+def pack_nodes(nodes, n):
+    """Node records in Node<N>::serialize field order (Node.h:57-64:
+    g, f, pos[N], parenti; little-endian, 12 + 2N bytes each)."""
+    arr = _c_nodes(nodes)
+    cap = (12 + 2 * n) * len(nodes)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    ln = ctypes.c_int64()
+    check(lib().pastar_wire_pack_nodes(arr, len(nodes), n, out, cap, ctypes.byref(ln)))
+    return out.raw[:ln.value]
+
+
+def unpack_nodes(data, n):
+    data = bytes(data)
+    cap = len(data) // (12 + 2 * n)
+    arr = (nat.pastar_node * max(cap, 1))()
+    c = ctypes.c_int()
+    check(lib().pastar_wire_unpack_nodes(data, len(data), n, arr, cap, ctypes.byref(c)))
+    return [Node(tuple(arr[k].pos[:n]), arr[k].g, arr[k].f, arr[k].parent_mask) for k in range(c.value)]
+
+
 def _c_coord(coord):
     c = (ctypes.c_uint16 * nat.MAX_SEQ)()
     for i, v in enumerate(coord):
