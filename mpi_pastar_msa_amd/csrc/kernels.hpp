@@ -679,7 +679,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
 // All lanes of the wave must call it.
-template <int KW, int PFS = 1, typename PP>
+// SH = false: the one-shard search (no owner routing, no outbox code)
+template <int KW, int PFS = 1, bool SH = true, typename PP>
 __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, StepStats *st, int f0, int w,
                                             bool valid, bool local, int owner, const uint64_t (&ck)[KW], int g, int h,
                                             int m, unsigned &claimed, unsigned &ovf,
@@ -753,7 +754,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
         }
     }
     queue_append(a, global, bucket_of(f, f0, w), e, st, remote_in);
-    if (P.n_shards > 1) {
+    if (SH && P.n_shards > 1) {
         const bool remote = valid && !local;
         Remote<KW> rec;
 #pragma unroll
@@ -1099,7 +1100,9 @@ __device__ __forceinline__ Entry batch_entry_at(const SearchArgs &a, const SelVi
 // expand every entry of the batch (worker_inner's dequeue, closed check and
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
 // (PAStar::enqueue + conditional_enqueue, :219-237).
-template <int N, int KW>
+// SH = false: instantiated for the one-shard search, whose launches never
+// route a child to another shard (the sharded protocol launches SH = true)
+template <int N, int KW, bool SH = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_waves_per_eu(N, KW)))) void expand_kernel(SearchArgs a)
 {
     constexpr int SW = slot_words<KW>();
@@ -1128,7 +1131,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // (the fused select of the first step)
     // a batch of at most one entry per block (N = 4): each block takes one
     // parent and starts its chain with the two-level pass below
-    const bool single = N == 4 && KW == 1 && nb > 0 && nb <= gridDim.x && P.n_shards == 1 && view.depth > 2;
+    const bool single = N == 4 && KW == 1 && nb > 0 && nb <= gridDim.x && (!SH || P.n_shards == 1) && view.depth > 2;
     const unsigned long long eff_per_block = single ? 1 : per_block;
     const unsigned long long nact =
         nb ? ((nb + eff_per_block - 1) / eff_per_block < gridDim.x ? (nb + eff_per_block - 1) / eff_per_block
@@ -1337,7 +1340,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 } else {
                     child_key<N, KW>(P, n, par_.key, m, ck);
                 }
-                if (P.n_shards > 1) {
+                if (SH && P.n_shards > 1) {
                     int cp[Parent<N, KW>::NMAX];
 #pragma unroll
                     for (int i = 0; i < Parent<N, KW>::NMAX; i++)
@@ -1346,7 +1349,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 }
             }
             BPHASE(8)
-            route_child<KW, kPfSlots>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp,
+            route_child<KW, kPfSlots, SH>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp,
                                       false, has_pf && r == 0, pf);
             BPHASE(9)
         }
@@ -1463,7 +1466,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             lq_count[nxt] = 0;
         lds_barrier();
         if constexpr (kTwoLevel) {
-            if (cnt == 1 && lvl + 1 < depth && P.n_shards == 1) {
+            if (cnt == 1 && lvl + 1 < depth && (!SH || P.n_shards == 1)) {
                 // one parent: this level and the next in one pass.  The next
                 // level of the one-level pass would expand exactly this
                 // parent's improved children below f_limit (its whole queue);
@@ -1582,7 +1585,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 }
                 const LocalPush<KW> lq_next2{lvl + 2 < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap,
                                              outq, &out_n};
-                route_child<KW, kPfSlots>(a, P, st, f0, w, v2, true, P.shard, tk, g2, h2, m, claimed, ovf, lq_next2,
+                route_child<KW, kPfSlots, SH>(a, P, st, f0, w, v2, true, P.shard, tk, g2, h2, m, claimed, ovf, lq_next2,
                                           false, v2, pf);
                 BLK_COUNT(2, 1)
                 lds_barrier();

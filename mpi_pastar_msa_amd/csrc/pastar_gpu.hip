@@ -494,6 +494,7 @@ struct Ops {
     void (*expand_api)(dim3, dim3, hipStream_t, const DevProblem *, const pastar_node *, int, const int64_t *, int,
                        pastar_node *, int32_t *, int32_t *);
     void (*expand)(dim3, dim3, hipStream_t, const SearchArgs &);
+    void (*expand_one_shard)(dim3, dim3, hipStream_t, const SearchArgs &);
     void (*insert_remote)(dim3, dim3, hipStream_t, const SearchArgs &, const void *, unsigned long long);
     void (*walk)(hipStream_t, const DevProblem *, const uint64_t *, uint64_t, const uint64_t *, int, int, int32_t *,
                  uint64_t *, int *, const int *);
@@ -510,7 +511,11 @@ struct Impl {
     }
     static void expand(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a)
     {
-        hipLaunchKernelGGL((expand_kernel<N, KW>), g, b, 0, s, a);
+        hipLaunchKernelGGL((expand_kernel<N, KW, true>), g, b, 0, s, a);
+    }
+    static void expand_one_shard(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a)
+    {
+        hipLaunchKernelGGL((expand_kernel<N, KW, false>), g, b, 0, s, a);
     }
     static void insert_remote(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a, const void *recs,
                               unsigned long long count)
@@ -538,7 +543,7 @@ struct Impl {
     {
         hipLaunchKernelGGL((lookup_kernel<KW>), dim3(1), dim3(1), 0, s, t, cm, key, out);
     }
-    static Ops ops() { return Ops{expand_api, expand, insert_remote, walk, lookup, tail}; }
+    static Ops ops() { return Ops{expand_api, expand, expand_one_shard, insert_remote, walk, lookup, tail}; }
 };
 
 template <int KW>
@@ -1262,7 +1267,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         constexpr int kStepRuns[kRuns] = {4, 8, 16, 32};
         auto enqueue_steps = [&](int S) -> hipError_t {
             for (int k = 0; k < S; k++)
-                ops.expand(expand_grid, blk, c->stream, a);
+                ops.expand_one_shard(expand_grid, blk, c->stream, a);
             return hipGetLastError();
         };
         bool use_graph = !cfg.eager;
