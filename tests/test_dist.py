@@ -266,3 +266,63 @@ def test_bench_rccl_id_rendezvous():
     port = free_port() - 17
     res = run_ranks(2, _share_id, port)
     assert res[0] == res[1] == bytes(range(128))
+
+
+def _wire_nodes(rank, n, count):
+    import random
+    from mpi_pastar_msa_amd import Node
+    rng = random.Random(1000 + rank)
+    out = []
+    for _ in range(count):
+        pos = tuple(rng.randrange(0, 300) for _ in range(n))
+        g = sum(pos) * 30 + rng.randrange(0, 90)
+        out.append(Node(pos, g, g + rng.randrange(0, 400), rng.randrange(1, 1 << n)))
+    return out
+
+
+def _wire_exchange(rank, world, n, count):
+    """The reference's message path between ranks (PAStarSender.cpp:54-62 ->
+    PAStarMessageProcesser.cpp:40-50): each rank routes its nodes to their
+    owners (Coord::get_id, z-order / 12), packs every destination's nodes in
+    Node::serialize field order, frames them as pastar_lz4_en does, and
+    sends the frame; the owner decodes and unpacks.  gloo carries the bytes
+    here in place of MPI."""
+    from mpi_pastar_msa_amd import get_id, lz4_dec, lz4_en, pack_nodes, unpack_nodes
+    mine = _wire_nodes(rank, n, count)
+    per = {d: [x for x in mine if get_id(x.pos, world) == d] for d in range(world)}
+    reqs, keep = [], []
+    for d in range(world):
+        if d == rank:
+            continue
+        frame = lz4_en(pack_nodes(per[d], n))
+        t_len = torch.tensor([len(frame)], dtype=torch.int64)
+        t_buf = torch.frombuffer(bytearray(frame), dtype=torch.uint8)
+        keep += [t_len, t_buf]
+        reqs.append(dist.isend(t_len, d))
+        reqs.append(dist.isend(t_buf, d))
+    got = list(per[rank])
+    for s in range(world):
+        if s == rank:
+            continue
+        t_len = torch.zeros(1, dtype=torch.int64)
+        dist.recv(t_len, s)
+        t_buf = torch.zeros(int(t_len.item()), dtype=torch.uint8)
+        dist.recv(t_buf, s)
+        raw = lz4_dec(t_buf.numpy().tobytes())
+        assert raw[-1:] == b"\0"
+        got += unpack_nodes(raw[:-1], n)
+    for r in reqs:
+        r.wait()
+    assert all(get_id(x.pos, world) == rank for x in got)
+    # every rank regenerates what the others sent it
+    want = [x for s in range(world) for x in _wire_nodes(s, n, count) if get_id(x.pos, world) == rank]
+    key = lambda x: (x.pos, x.g, x.f, x.parenti)
+    assert sorted(map(key, got)) == sorted(map(key, want))
+    return len(got)
+
+
+@pytest.mark.parametrize("world,n", [(2, 4), (3, 8)])
+def test_wire_frame_exchange_between_ranks(world, n):
+    counts = run_ranks(world, _wire_exchange, n, 3000)
+    assert sum(counts) == world * 3000
+    assert all(c > 0 for c in counts)
