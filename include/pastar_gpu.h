@@ -52,6 +52,10 @@ extern "C" {
 #define PASTAR_ENOTFOUND (-5)
 #define PASTAR_ECOMM (-6)    /* RCCL failure                          */
 #define PASTAR_ESTATE (-7)   /* call out of order                     */
+#define PASTAR_EDEVWAIT (-8) /* a bounded wait ran out: a wave's wait on
+                                another wave on the device, or the host's
+                                wait for a launch to report its end; the
+                                call's results are discarded             */
 
 /* Coord hash types, same numbering as the reference's hashType enum
  * (Coord.h:29): HashFZorder, HashPZorder, HashFSum, HashPSum. */
@@ -243,7 +247,12 @@ int pastar_gpu_alignment(pastar_ctx *ctx, char *rows, int stride, int *cols);
  * reference's classes).  One node record serves both lists, so a node is in
  * at most one of them; ties on g keep the smaller parent mask (the batched
  * engine's rule) where the reference keeps the first found.  Single shard.
- * A search (pastar_gpu_search) reuses the buffers and ends the session. */
+ * A search (pastar_gpu_search) reuses the buffers and ends the session.
+ * Deviation from PriorityList alone: pastar_gpu_open_enqueue always makes
+ * PAStar::enqueue's ClosedList check (PAStar.cpp:226-232), so a node cannot
+ * be put into the OpenList while a ClosedList record with g <= its g exists;
+ * the reference's PriorityList::conditional_enqueue would accept it, and no
+ * call site of the reference asks that (each checks or erases first). */
 
 /* PAStar construction: empty lists (opts: table_slots_log2, pool_entries,
  * subqueue_entries, band; zeros = defaults). */
@@ -279,6 +288,19 @@ int pastar_gpu_lists_erase(pastar_ctx *ctx, const uint16_t *pos, int which, int 
 
 /* Reopenings since pastar_gpu_lists_reset (nodes_reopen, PAStar.cpp:232). */
 int pastar_gpu_lists_reopened(pastar_ctx *ctx, int64_t *reopened);
+
+/* ---- device self-tests (no counterpart in the reference) ----
+ * The open list hands chunk ids from the lane that reserves a range to the
+ * lanes that store into it (the device-side form of PAStar::enqueue's
+ * inserts, PAStar.cpp:219-237, run by many workgroups at once).
+ * scenario 0: two workgroups reserve ranges of two f buckets in crossed
+ *   order and store first into the bucket where they came second; must end
+ *   with every entry in place (info[0] = wrong entries, info[1] = checked).
+ * scenario 1: a store into a chunk nobody opened, its wait bounded at 64
+ *   polls from the host: the kernel ends normally and the call returns
+ *   PASTAR_EDEVWAIT naming the site.
+ * After pastar_gpu_build_heuristic; ends any list session. */
+int pastar_gpu_selftest_queue(pastar_ctx *ctx, int scenario, int64_t *info);
 
 /* ---- MPI-compatible wire frame -------------------------
  * The reference's inter-rank message frame, byte-identical to what its

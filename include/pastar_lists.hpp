@@ -4,16 +4,25 @@
 //   reference                                    here
 //   -------------------------------------------  ------------------------------
 //   PriorityList<N> (PriorityList.h:52-122)      pastar::PriorityList<N>
-//     dequeue, conditional_enqueue,                same names, same meaning;
-//     get_highest_priority, find, erase,           the list lives on the device
-//     size, empty                                  (pastar_gpu_open_*)
+//     dequeue, conditional_enqueue,                same names and return
+//     get_highest_priority, find, erase,           values; the list lives on
+//     size, empty                                  the device (pastar_gpu_open_*)
 //   ClosedList[tid] std::map (PAStar.cpp:92)     pastar::ClosedList<N>
 //     find, erase, size                            (pastar_gpu_lists_*)
 //   PAStar::enqueue (PAStar.cpp:219-237)         PriorityList::enqueue(vector)
 //
-// One device node record serves both lists (see pastar_gpu.h): dequeue moves
-// its node into the ClosedList (worker_inner's `ClosedList[pos] = current`,
-// PAStar.cpp:351, which can never refuse a node the OpenList just gave up).
+// Two deviations from the reference's classes, both forced by one device node
+// record serving both lists (see pastar_gpu.h):
+//  - dequeue moves its node into the ClosedList (worker_inner's
+//    `ClosedList[pos] = current`, PAStar.cpp:351, which can never refuse a
+//    node the OpenList just gave up);
+//  - conditional_enqueue includes PAStar::enqueue's ClosedList check
+//    (PAStar.cpp:226-232): a node that sits in the ClosedList with g <= the
+//    new g is discarded, one with a larger g leaves the ClosedList (a
+//    reopening).  The reference's PriorityList alone would hold such a node
+//    in both lists; the reference never asks it to: each of its calls of
+//    conditional_enqueue comes behind that check or an erase (PAStar.cpp:
+//    226-234, 531-537; AStar.cpp:86-93).
 // Errors throw pastar::Error with the C-ABI status and message.
 #ifndef PASTAR_LISTS_HPP
 #define PASTAR_LISTS_HPP
@@ -71,13 +80,18 @@ class PriorityList {
         return cnt;
     }
 
-    // PriorityList.h:104-113 (with the ClosedList check of PAStar::enqueue):
-    // true when n entered the OpenList
-    bool conditional_enqueue(const pastar_node &n)
+    // PriorityList.h:104-113.  Returns what the reference returns: true
+    // whether n was inserted, replaced a worse record, or was discarded as
+    // not better (:109-110 returns true for that too; insert and modify
+    // cannot fail there).  *entered (optional) tells the cases apart: true
+    // when n is now the OpenList's record of its coordinate.
+    bool conditional_enqueue(const pastar_node &n, bool *entered = nullptr)
     {
         int32_t added = 0;
         check(pastar_gpu_open_enqueue(ctx_, &n, 1, &added, nullptr));
-        return added != 0;
+        if (entered)
+            *entered = added != 0;
+        return true;
     }
 
     // PAStar::enqueue (PAStar.cpp:219-237) over a batch; returns the nodes

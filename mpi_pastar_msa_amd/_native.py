@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libpastar_gpu.so")
 
 MAX_SEQ = 16
-OK, EINVAL, ENODEV, ENOMEM, EIO, ENOTFOUND, ECOMM, ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
+OK, EINVAL, ENODEV, ENOMEM, EIO, ENOTFOUND, ECOMM, ESTATE, EDEVWAIT = 0, -1, -2, -3, -4, -5, -6, -7, -8
 
 HASH_TYPES = {"FZORDER": 0, "PZORDER": 1, "FSUM": 2, "PSUM": 3}
 HASH_NAMES = {0: "Full-Zorder", 1: "Partial-Zorder", 2: "Full-Sum", 3: "Partial-Sum"}
@@ -149,6 +149,7 @@ SIGNATURES = {
     "pastar_gpu_lists_erase": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16), ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int)]),
     "pastar_gpu_lists_reopened": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_gpu_selftest_queue": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
     # MPI-compatible wire frame (host only)
     "pastar_wire_frame_bound": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "pastar_wire_frame_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,

@@ -20,14 +20,19 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # -ffp-contract=off keeps the host weight pipeline in plain IEEE single
 # arithmetic (no FMA contraction), as the reference's g++ build computes it.
+# no packed-FP32 instructions (hipcc -O3 forms them from ordinary float code;
+# the engine's device arithmetic is integer, the flag keeps it that way for
+# any float code the compiler meets; the host pass does not know the feature
+# and says so, harmlessly)
 COMMON = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+          "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 # diagnostics builds, e.g. PASTAR_HIPCC_FLAGS=-DPASTAR_PHASE_TIMERS (block-0
 # phase timers of the expand kernel, read with PASTAR_TIMING_MASK=5)
 COMMON += os.environ.get("PASTAR_HIPCC_FLAGS", "").split()
 
 LIB_SOURCES = ["pastar_gpu.hip", "host_model.cpp", "wire.cpp"]
-LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp", "solo.hpp", "lists.hpp"]
+LIB_DEPS = LIB_SOURCES + ["device.hpp", "kernels.hpp", "host_model.hpp", "solo.hpp", "lists.hpp", "selftest.hpp"]
 
 
 def _stale(target, deps):

@@ -36,6 +36,18 @@ constexpr uint64_t kMark = 1ull << 63;  // key word written / occupied
 constexpr int kMaxProbe = 1 << 16;
 constexpr int kIntMax = 0x7fffffff;
 
+// Bounded device waits.  A wave waits on another wave in three places: a
+// queue store on the chunk id its reserver publishes (queue_store), a relax on
+// the tail words of a multi-word key being published (relax), and a PairAlign
+// band on the band below it.  Each waits at most a fixed number of polls;
+// one that runs out ORs its site into the context's fault word and carries
+// on without the datum (the entry is dropped, the cell is garbage), so every
+// kernel still ends, and the host turns a non-zero fault word into
+// PASTAR_EDEVWAIT naming the site.
+enum { kSiteQueueStore = 1, kSiteRelaxTail = 2, kSitePairAlign = 4, kSiteSelftest = 8 };
+constexpr unsigned kSpinLimit = 1u << 22;  // polls of ~0.1-1 us each
+
+
 struct DevProblem {
     int n, npairs, kw, alpha;
     int gap_open, gap_ext, gap_gap;
@@ -197,8 +209,9 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
     }
 }
 
-// Relax (key, g, parent mask) into the node table.  Returns the slot (or -1
-// when the probe limit is hit) and sets `improved` when g is strictly better
+// Relax (key, g, parent mask) into the node table.  Returns the slot (-1
+// when the probe limit is hit, -2 when a key's tail words were not published
+// within kSpinLimit re-reads) and sets `improved` when g is strictly better
 // than every g recorded for the key so far; `claimed` when the slot is new.
 //
 // Concurrency: slots are never freed, and every key word goes 0 -> final
@@ -236,6 +249,7 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
     else
         idx = probe_start<KW>(key, cap_mask);
     int probe = 0;
+    unsigned tail_polls = 0;
     // the prefetched slots: skip those holding other keys (key word 0 set
     // and different), and start at the first empty or candidate one with
     // its prefetched words (constant indices only: no register array is
@@ -319,8 +333,14 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
                 pending |= (v == 0);
                 same &= (v == key[w]);
             }
-            if (pending)
-                continue;  // tail still being published: re-read this slot
+            if (pending) {
+                // tail still being published (by a claimant that is past its
+                // CAS and stores the tail next): re-read this slot, a bounded
+                // number of times
+                if (++tail_polls > kSpinLimit)
+                    return -2;
+                continue;
+            }
             if (!same) {
                 idx = (idx + 1) & cap_mask;
                 probe++;

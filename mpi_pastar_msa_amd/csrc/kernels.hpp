@@ -82,7 +82,8 @@ typedef int pa_v4i __attribute__((ext_vector_type(4), aligned(8)));
 template <bool SUB_LDS, bool WRITE_H, bool EQ_GAPS>
 __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const DevProblem *__restrict__ Pp,
                                                                        int32_t *__restrict__ H,
-                                                                       int2 *__restrict__ HC)
+                                                                       int2 *__restrict__ HC,
+                                                                       int *__restrict__ fault, unsigned spin_limit)
 {
     static_assert(kPaChunk == 8, "the progress handshake runs every 8 steps, once per chunk");
     const DevProblem &P = *Pp;
@@ -156,8 +157,19 @@ __global__ __launch_bounds__(64 * kPaWaves) void pairalign_wave_kernel(const Dev
                 // lane 63 reads column L2 - t of band - 1's top row, written
                 // by its lane 0 at its step t + 63; one check covers 8 steps
                 const int need = ((band - 1) << 16) | (t0 + 71 < nsteps ? t0 + 71 : nsteps);
-                while (__hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+                // (band - 1 runs on another wave of this workgroup and waits
+                // only on band - 2, ..., band 0 on nothing; bounded all the same:
+                // a wait that runs out flags the fault word and goes on with
+                // whatever the row holds)
+                unsigned poll = 0;
+                while (__hip_atomic_load(prev_progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                    if (++poll > spin_limit) {
+                        if (lane == 0)
+                            atomicOr(fault, (int)kSitePairAlign);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
+                }
                 asm volatile("" ::: "memory");  // the row reads below stay after the wait
             }
             const int j0 = j;  // this lane's column at step t0
@@ -431,7 +443,7 @@ __host__ __device__ inline int fail_bits(unsigned long long near, unsigned long 
 // block reads slows every launch), then the last block's diagnostics.
 struct Ctl {
     // ---- read by every block, written by select ----
-    int status;     // 0 running, 1 done, 2 capacity exhausted, 3 step limit
+    int status;     // 0 running, 1 done, 2 capacity exhausted, 3 step limit, 4 a bounded device wait ran out
     int band_log2;  // bucket width = 2^band_log2
     int f0;         // f of bucket 0 (h of the origin)
     int batch_b;    // first bucket of the current batch
@@ -474,7 +486,8 @@ struct Ctl {
     // {blocks, sum levels, max levels, sum rounds, max rounds, max ticks},
     // then continuation levels by parents: 1, 2..4, 5..16, more
     unsigned long long blk_stats[10];
-    int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step, pad1;
+    int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step;
+    int fault_sites;  // status 4: the kSite* bits select found in the fault word
     unsigned long long dbg_w, dbg_r;
 };
 
@@ -512,6 +525,8 @@ constexpr int kTraceSteps = 4096;
 struct SearchArgs {
     const DevProblem *P;
     Ctl *ctl;
+    int *fault;           // kSite* bits of waits that ran out (sticky until the host clears it)
+    unsigned spin_limit;  // polls a queue store waits for its chunk id (kSpinLimit; tests lower it)
     unsigned long long *stamps;  // [kArrive] start stamps of the first blocks
     int *trace;                  // debug: [kTraceSteps][8] per-step select trace (nullptr: off)
     uint64_t *table;
@@ -568,12 +583,33 @@ __device__ __forceinline__ int bucket_of(int f, int f0, int w)
     return b < 0 ? 0 : (b >= kBuckets ? kBuckets - 1 : (int)b);
 }
 
-// Write entry e at position p of sub-queue (b, sq).  The lane whose position
-// opens a chunk allocates it; the others wait for its publication (the
-// allocating wave reserved an earlier range, so it is resident and past its
-// reservation).  The chunk id is the only datum handed over, so the
-// publication is relaxed (an agent-scope release or acquire would write back
-// or invalidate the L2 on every append).
+// Reserve n consecutive positions of sub-queue (b, sq) (n <= kChunk; one
+// lane) and open every chunk whose first position falls in the reserved
+// range: its id is taken from the pool and published in the chunk table
+// before this lane does anything else.  A store into a chunk (queue_store)
+// waits for that publication, so what a store waits on is always one lane
+// that has finished its cursor add and whose next instructions are the pool
+// add and the publication, with no wait of its own in between: stores can
+// form no circular wait, in whatever order blocks reserve ranges of several
+// buckets and store into them.  (The chunk id is the only datum handed over,
+// so the publication is relaxed: an agent-scope release or acquire would
+// write back or invalidate the L2 on every append.)
+__device__ __forceinline__ unsigned long long queue_reserve(const SearchArgs &a, int b, int sq, unsigned n)
+{
+    const unsigned long long base = atomicAdd(&a.q->W[b][sq], (unsigned long long)n);
+    for (unsigned long long k = (base + kChunk - 1) >> kChunkLog2; (k << kChunkLog2) < base + n && k < a.maxch; k++) {
+        const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
+        const uint32_t c = id < a.pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
+        __hip_atomic_store(a.chunk_tab + ((size_t)b * kSub + sq) * a.maxch + k, c, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return base;
+}
+
+// Write entry e at position p (reserved by queue_reserve) of sub-queue
+// (b, sq).  The chunk's id is read from the chunk table; a position whose
+// chunk's reserver has not published yet waits for it, at most
+// a.spin_limit polls (see queue_reserve: the reserver never waits).
 __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, unsigned long long p, const Entry &e,
                                             StepStats *st)
 {
@@ -585,14 +621,17 @@ __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, 
         return;
     }
     uint32_t *tp = a.chunk_tab + ((size_t)b * kSub + sq) * maxch + k;
-    uint32_t c = 0;
-    if (off == 0) {  // the opener knows the id: no read-back
-        const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
-        c = id < a.pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
-        __hip_atomic_store(tp, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == 0) {
+        for (unsigned poll = 0; poll < a.spin_limit && c == 0; poll++) {
+            __builtin_amdgcn_s_sleep(1);
+            c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (c == 0) {  // the wait ran out: flag it, drop the entry
+            atomicOr(a.fault, (int)kSiteQueueStore);
+            return;
+        }
     }
-    while (c == 0 && (c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
-        __builtin_amdgcn_s_sleep(1);
     if (c == kNoChunk) {
         atomicAdd(&st->ovf_near, 1ull);
         return;
@@ -616,7 +655,7 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
         const uint64_t m = __ballot(pred && b == bl) & pending;
         unsigned long long base = 0;
         if (lane == leader) {
-            base = atomicAdd(&a.q->W[bl][sq], (unsigned long long)__popcll(m));
+            base = queue_reserve(a, bl, sq, (unsigned)__popcll(m));
             // entries from other shards may land below this shard's minimum
             if (may_lower && bl < ld_agent(&a.ctl->cur_b))
                 atomicMin(&a.ctl->cur_b, bl);
@@ -663,6 +702,7 @@ struct LocalPush {
 };
 
 constexpr int kOutCap = 1024;  // entries a block defers to its final append
+static_assert(kOutCap <= kChunk, "one reservation opens at most one chunk");
 
 // A group leader's verdict (0, 1, 2) to every lane of its group, by two
 // ballots (no LDS round trip; the leader lane is per group, not uniform)
@@ -692,6 +732,8 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
     if (valid && local) {
         slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre);
         if (slot < 0) {
+            if (slot == -2)
+                atomicOr(a.fault, (int)kSiteRelaxTail);
             ovf++;
             improved = false;
         }
@@ -812,7 +854,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     static_assert(kStatRows == 64, "one wave sums the stat rows");
     static_assert(kWin >= kWide, "the first window covers a batch's buckets");
     static_assert(kRanges == 128 && kSub % 2 == 0, "one wave cuts the batch, two ranges per lane");
-    __shared__ int found, found2, goal_s, cur_s, fail_s;
+    __shared__ int found, found2, goal_s, cur_s, fail_s, fault_s;
     __shared__ unsigned long long wv[kBlock], rv[kBlock];
     __shared__ unsigned long long sums[kStFields], ovf[3];
     const bool prof = v.timing & 2;
@@ -869,6 +911,8 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     } else if (tid == kStatRows + 5) {
         found = kBuckets;
         found2 = kBuckets;
+    } else if (tid == kStatRows + 6) {
+        fault_s = ld_agent(a.fault);
     }
     __syncthreads();
     PHASE(0)
@@ -887,7 +931,11 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
             ctl->fail_mask |= fm;
             ctl->status = 2;
         }
-        fail_s = fm;
+        if (fault_s) {  // a bounded device wait ran out: the search's state is no longer exact
+            ctl->fault_sites = fault_s;
+            ctl->status = 4;
+        }
+        fail_s = fm | fault_s;
     }
     const int goal = goal_s;
     const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
@@ -1644,8 +1692,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             }
             __syncthreads();
             const int sq = blockIdx.x % kSub;
+            // (each reserving lane also opens the chunks that start in its
+            // range, before any store of the block: queue_reserve)
             if (threadIdx.x < kWin && fb_cnt[threadIdx.x])
-                fb_base[threadIdx.x] = atomicAdd(&a.q->W[bmin + threadIdx.x][sq], (unsigned long long)fb_cnt[threadIdx.x]);
+                fb_base[threadIdx.x] = queue_reserve(a, bmin + threadIdx.x, sq, fb_cnt[threadIdx.x]);
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < kPer; k++) {

@@ -6,7 +6,9 @@
 //
 // One table slot holds a node of both lists (Open U Closed): best = g << 32 |
 // parent mask, aux = closed g | h << 32.  A node is
-//   open    iff best.g < closed g   (it has a live queue entry: f = best.g + h)
+//   open    iff best.g < closed g   (it has a live queue entry: f = best.g + h;
+//                                    closed g is INT_MAX: an enqueue that
+//                                    improves a closed node resets it)
 //   closed  iff closed g <= best.g  (closed g != INT_MAX)
 //   absent  iff its slot is unclaimed or best == ~0 (erased)
 #pragma once
@@ -75,11 +77,18 @@ __global__ __launch_bounds__(kListThreads) void lists_enqueue_kernel(SearchArgs 
         slot = relax<KW, 1>(a.table, a.cap_mask, key, nd.g, nd.parent_mask, nd.f - nd.g, improved, claimed, false,
                             SlotWords<KW, 1>{});
         if (slot < 0) {
+            if (slot == -2)
+                atomicOr(a.fault, (int)kSiteRelaxTail);
             improved = false;
             atomicAdd(&out[1], 1ull);
         } else if (improved) {
-            const int closed = (int)(uint32_t)a.table[(uint64_t)slot * SW + KW + 1];
-            if (closed != kIntMax)
+            // a ClosedList node improved: it leaves the ClosedList here
+            // (ClosedList[tid].erase, PAStar.cpp:230) and is counted once
+            // (nodes_reopen, :231), whichever of several improving entries
+            // of one batch gets there first; its later dequeue then closes
+            // an open node and counts nothing
+            int *closed = reinterpret_cast<int *>(a.table + (uint64_t)slot * SW + KW + 1);
+            if (*closed != kIntMax && atomicExch(closed, kIntMax) != kIntMax)
                 atomicAdd(&out[0], 1ull);
         }
         added[i] = improved ? 1 : 0;
@@ -205,6 +214,26 @@ __global__ __launch_bounds__(kListThreads) void lists_dequeue_kernel(SearchArgs 
                 out[at] = nd;
             }
             __syncthreads();
+            // entries ahead of the first live one are never looked at again:
+            // each sub-queue's R moves past its leading run of dead entries
+            // (stale, closed, or taken just now), so a bucket that drains
+            // one node per call is not rescanned from its start every time
+            if (tid < kSub) {
+                const unsigned long long end = r0[tid] + (n_sq[tid + 1] - n_sq[tid]);
+                unsigned long long r = r0[tid];
+                for (; r < end; r++) {
+                    Entry e;
+                    if (!queue_entry(a, b, tid, r, e))
+                        continue;  // reserved, never written: dead
+                    const uint64_t *s = a.table + (uint64_t)e.slot * SW;
+                    const uint64_t best = ld_agent(&s[KW]), aux = ld_agent(&s[KW + 1]);
+                    const int g = (int)(best >> 32), h = (int)(aux >> 32);
+                    if (best != ~0ull && g + h == e.f && g < (int)(uint32_t)aux)
+                        break;  // live: stays
+                }
+                if (r != r0[tid])
+                    st_agent(&a.q->R[b][tid], r);
+            }
         }
         break;
     }

@@ -34,6 +34,7 @@
 #include "pastar_gpu.h"
 #include "lists.hpp"
 #include "solo.hpp"
+#include "selftest.hpp"
 
 using namespace pastar;
 using namespace pastar::dev;
@@ -249,6 +250,8 @@ struct pastar_ctx {
     // shard with an RCCL communicator of its own (the protocol at world 1)
     std::unique_ptr<Transport> tr;
     DevBuf<int64_t> xred;           // RCCL staging of small collectives
+    DevBuf<int> fault;              // kSite* bits of bounded device waits that ran out (kernels.hpp)
+    unsigned spin_limit = kSpinLimit;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
@@ -487,6 +490,50 @@ int check_launch()
     return PASTAR_OK;
 }
 
+const char *fault_site_name(int sites)
+{
+    if (sites & kSiteQueueStore)
+        return "open-list chunk hand-over (queue_store)";
+    if (sites & kSiteRelaxTail)
+        return "node-table key publication (relax)";
+    if (sites & kSitePairAlign)
+        return "PairAlign band hand-over";
+    if (sites & kSiteSelftest)
+        return "self-test handshake";
+    return "unknown site";
+}
+
+// A bounded device wait that ran out leaves its site in the context's fault
+// word: report it as PASTAR_EDEVWAIT and clear the word (the stream is idle).
+int report_fault(pastar_ctx *c, int sites)
+{
+    (void)hipMemset(c->fault.p, 0, sizeof(int));
+    return fail(PASTAR_EDEVWAIT, "a device wait ran out of its bound at: %s (sites 0x%x); results discarded",
+                fault_site_name(sites), sites);
+}
+
+// Read the fault word after the stream has drained (calls outside the search,
+// whose select reads the word on the device).
+int check_fault(pastar_ctx *c)
+{
+    int sites = 0;
+    HIP_TRY(hipMemcpy(&sites, c->fault.p, sizeof(int), hipMemcpyDeviceToHost));
+    return sites ? report_fault(c, sites) : PASTAR_OK;
+}
+
+// Longest the host waits for one replay or one LDS-resident launch to report
+// completion (PASTAR_WAIT_TIMEOUT_S, default 600 s), after which the call
+// fails instead of polling forever.
+double host_wait_limit_s()
+{
+    static const double lim = [] {
+        const char *e = std::getenv("PASTAR_WAIT_TIMEOUT_S");
+        const double v = e && *e ? std::atof(e) : 600.0;
+        return v > 0 ? v : 600.0;
+    }();
+    return lim;
+}
+
 // ---------------------------------------------------------------------------
 // Per-(N, KW) dispatch
 // ---------------------------------------------------------------------------
@@ -660,6 +707,8 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
     PA_TRY(setup_problem(c.get(), p));
+    PA_TRY(c->fault.alloc(1));
+    HIP_TRY(hipMemset(c->fault.p, 0, sizeof(int)));
     {
         // load the code object now (the runtime loads it at the first use of
         // one of its kernels): a context's first search then pays only its
@@ -749,7 +798,7 @@ static int launch_pairalign(pastar_ctx *c, bool write_h)
                                  : (const void *)pairalign_wave_kernel<false, false, false>));
     if (lds > 64 * 1024)
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p};
+    void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p, (void *)&c->fault.p, (void *)&c->spin_limit};
     HIP_TRY(hipLaunchKernel(fn, dim3(c->npairs), dim3(64 * kPaWaves), args, lds, c->stream));
     PA_TRY(check_launch());
     // the search and h run on the same stream, so the search-form tables
@@ -794,6 +843,7 @@ int pastar_gpu_pair_table(pastar_ctx *c, int pair, int32_t *out)
     HIP_TRY(hipSetDevice(c->device));
     if (!c->plain_h_ready) {
         PA_TRY(launch_pairalign(c, true));
+        PA_TRY(check_fault(c));
         c->plain_h_ready = true;
         c->hc_built = true;
     }
@@ -832,6 +882,7 @@ int pastar_gpu_h(pastar_ctx *c, const uint16_t *pos, int count, int32_t *out)
     hipLaunchKernelGGL(h_kernel, dim3((count + 255) / 256), dim3(256), 0, c->stream, c->dP.p, dpos.p, count, dout.p);
     PA_TRY(check_launch());
     HIP_TRY(hipStreamSynchronize(c->stream));
+    PA_TRY(check_fault(c));
     HIP_TRY(hipMemcpy(out, dout.p, (size_t)count * 4, hipMemcpyDeviceToHost));
     return PASTAR_OK;
 }
@@ -878,6 +929,7 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
                           down.p, dsrc.p);
     PA_TRY(check_launch());
     HIP_TRY(hipStreamSynchronize(c->stream));
+    PA_TRY(check_fault(c));
     if (total) {
         if (out)
             HIP_TRY(hipMemcpy(out, dout.p, sizeof(pastar_node) * (size_t)total, hipMemcpyDeviceToHost));
@@ -1191,6 +1243,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     SearchArgs a{};
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
+    a.fault = c->fault.p;
+    a.spin_limit = c->spin_limit;
     a.stamps = c->stamps.p;
     DevBuf<int> trace;
     a.trace = nullptr;
@@ -1380,9 +1434,15 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // wait for a replay by watching the tail's completion word (its last
         // store) rather than for the stream's completion signal; the stream is
         // polled too, so a failure ends the wait with its error
+        bool wait_timed_out = false;
         auto wait_tail = [&]() -> hipError_t {
+            const double t_wait = now_s();
             for (unsigned spin = 1; *done != ta.ticket; spin++) {
                 if ((spin & 255) == 0) {
+                    if ((spin & 0xfffff) == 0 && now_s() - t_wait > host_wait_limit_s()) {
+                        wait_timed_out = true;
+                        return hipErrorNotReady;
+                    }
                     const hipError_t q = hipStreamQuery(c->stream);
                     if (q == hipSuccess && *done == ta.ticket)
                         break;
@@ -1414,7 +1474,11 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             if (e == hipSuccess)
                 e = wait_tail();
             if (e != hipSuccess) {
-                rc = fail(PASTAR_ENODEV, "search steps failed: %s", hipGetErrorString(e));
+                if (wait_timed_out)
+                    rc = fail(PASTAR_EDEVWAIT, "the device did not report a replay's end within %.0f s "
+                              "(PASTAR_WAIT_TIMEOUT_S); the launch is abandoned", host_wait_limit_s());
+                else
+                    rc = fail(PASTAR_ENODEV, "search steps failed: %s", hipGetErrorString(e));
                 break;
             }
             h = *c->h_ctl;
@@ -1431,6 +1495,8 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
             c->last_steps = h.steps;
         else if (rc == PASTAR_OK)  // a failed search may be retried on regrown buffers: drain first
             HIP_TRY(hipStreamSynchronize(c->stream));
+        if (wait_timed_out)
+            return rc;  // (nothing below may wait for the stream)
         c->graph_used = use_graph;
         PA_TRY(rc);
     } else {
@@ -1512,6 +1578,10 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     if (h.status == 3)
         return fail(PASTAR_ESTATE, "step limit %lld reached", (long long)cfg.max_steps);
+    if (h.status == 4) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return report_fault(c, h.fault_sites);
+    }
     // the goal and the open-list census (current entries left in the
     // queues; the table needs none: every claimed slot is a distinct node,
     // every first closing of a node is an expansion that is not a
@@ -1738,6 +1808,9 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     // stream is still polled, so a failed launch ends the wait with its error
     for (unsigned spin = 1; *done != a.ticket; spin++) {
         if ((spin & 255) == 0) {
+            if ((spin & 0xfffff) == 0 && now_s() - t0 > host_wait_limit_s())
+                return fail(PASTAR_EDEVWAIT, "the LDS-resident search did not report its end within %.0f s "
+                            "(PASTAR_WAIT_TIMEOUT_S); the launch is abandoned", host_wait_limit_s());
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipSuccess && *done == a.ticket)
                 break;
@@ -2310,6 +2383,8 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     a = SearchArgs{};
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
+    a.fault = c->fault.p;
+    a.spin_limit = c->spin_limit;
     a.stamps = c->stamps.p;
     a.table = c->table.p;
     a.cap_mask = c->nslots - 1;
@@ -2364,8 +2439,13 @@ int pastar_gpu_open_enqueue(pastar_ctx *c, const pastar_node *nodes, int count, 
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_flags, dflags, fb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_res, dres, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 16, &c->stats.p->ovf_near, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 32, c->fault.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const unsigned long long *r = reinterpret_cast<const unsigned long long *>(c->h_lists + off_res);
+    if (const int sites = *reinterpret_cast<const int *>(c->h_lists + off_res + 32)) {
+        c->lists_ready = false;
+        return report_fault(c, sites);
+    }
     if (r[1] || r[2] || r[3]) {
         c->lists_ready = false;  // a node was dropped: the lists are no longer exact
         return fail(PASTAR_ENOMEM, "OpenList capacity exhausted (table %llu, pool %llu, sub-queue %llu drops); "
@@ -2455,7 +2535,8 @@ static int lists_find_erase(pastar_ctx *c, const uint16_t *pos, int erase_which,
 {
     PA_TRY(lists_io(c, 128));
     uint8_t *d = c->lists_io.p;
-    std::memcpy(c->h_lists + 64, pos, 2 * PASTAR_MAX_SEQ);
+    std::memset(c->h_lists + 64, 0, 2 * PASTAR_MAX_SEQ);
+    std::memcpy(c->h_lists + 64, pos, sizeof(uint16_t) * (size_t)c->n);  // the caller's pos holds n coordinates
     HIP_TRY(hipMemcpyAsync(d + 64, c->h_lists + 64, 2 * PASTAR_MAX_SEQ, hipMemcpyHostToDevice, c->stream));
     const uint16_t *dpos = reinterpret_cast<const uint16_t *>(d + 64);
     unsigned long long *dres = reinterpret_cast<unsigned long long *>(d);
@@ -2511,6 +2592,57 @@ int pastar_gpu_lists_reopened(pastar_ctx *c, int64_t *reopened)
         return fail(PASTAR_EINVAL, "null argument");
     *reopened = c->lists_reopen;
     return PASTAR_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Device self-tests of the open list (selftest.hpp)
+// ===========================================================================
+extern "C" {
+
+int pastar_gpu_selftest_queue(pastar_ctx *c, int scenario, int64_t *info)
+{
+    if (!c || !info || scenario < 0 || scenario > 1)
+        return fail(PASTAR_EINVAL, "invalid arguments (scenario 0 or 1)");
+    info[0] = info[1] = 0;
+    // fresh, empty lists on the search's own buffers
+    PA_TRY(pastar_gpu_lists_reset(c, nullptr));
+    c->lists_ready = false;  // the queues below are no list session's
+    SearchArgs a = c->lists_args;
+    const int b1 = 3, b2 = 5;
+    PA_TRY(lists_io(c, 64));
+    unsigned *flags = reinterpret_cast<unsigned *>(c->lists_io.p);
+    unsigned long long *out = reinterpret_cast<unsigned long long *>(c->lists_io.p + 16);
+    HIP_TRY(hipMemsetAsync(c->lists_io.p, 0, 64, c->stream));
+    if (scenario == 0) {
+        // the handshake between the two workgroups: they are co-resident on
+        // an idle device, so it takes microseconds; bounded at ~1 s
+        hipLaunchKernelGGL(selftest_crossed_kernel, dim3(2), dim3(64), 0, c->stream, a, b1, b2, flags, 1u << 22);
+        PA_TRY(check_launch());
+        hipLaunchKernelGGL(selftest_crossed_check_kernel, dim3(1), dim3(64), 0, c->stream, a, b1, b2, out);
+        PA_TRY(check_launch());
+        HIP_TRY(hipMemcpyAsync(c->h_lists, out, 16, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        PA_TRY(check_fault(c));
+        const unsigned long long *r = reinterpret_cast<const unsigned long long *>(c->h_lists);
+        info[0] = (int64_t)r[0];
+        info[1] = (int64_t)r[1];
+        if (r[0])
+            return fail(PASTAR_ESTATE, "crossed reservations left %llu wrong entries of %llu", r[0], r[1]);
+        return PASTAR_OK;
+    }
+    // scenario 1: a cursor moved into a chunk nobody opened, and a store wait
+    // bounded at 64 polls: the stores must give up, flag the site, and the
+    // call must report PASTAR_EDEVWAIT
+    const unsigned long long lost = 8;
+    HIP_TRY(hipMemcpyAsync(&c->queues.p->W.d[0][b1], &lost, sizeof(lost), hipMemcpyHostToDevice, c->stream));
+    a.spin_limit = 64;
+    hipLaunchKernelGGL(selftest_lost_opener_kernel, dim3(1), dim3(64), 0, c->stream, a, b1);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->queues_clean_known = false;  // a cursor without its chunk: clear everything next time
+    return check_fault(c);
 }
 
 }  // extern "C"

@@ -348,6 +348,15 @@ class Engine:
         check(lib().pastar_gpu_search(self._ctx, ctypes.byref(self._so), ctypes.byref(r)))
         return SearchResult(*r.as_tuple())
 
+    def selftest_queue(self, scenario):
+        """pastar_gpu_selftest_queue: (wrong entries, entries checked); raises
+        NativeError(EDEVWAIT) when a bounded device wait ran out."""
+        if not self._ready:
+            self.init()
+        info = (ctypes.c_int64 * 4)()
+        check(lib().pastar_gpu_selftest_queue(self._ctx, int(scenario), info))
+        return info[0], info[1]
+
     def closed_lookup(self, coord):
         c = (ctypes.c_uint16 * MAX_SEQ)(*coord)
         out = nat.pastar_node()
@@ -396,7 +405,13 @@ def lz4_dec(frame):
     frame = bytes(frame)
     if len(frame) < 12:
         raise nat.NativeError(-1, "frame shorter than its header")  # PASTAR_EINVAL
+    total = int.from_bytes(frame[0:4], "little")
     orig = int.from_bytes(frame[8:12], "little")
+    # the header is untrusted: an LZ4 block expands at most 255x, so a length
+    # beyond that (or a frame shorter than it says) is rejected before any
+    # buffer is sized from it
+    if total > len(frame) or total < 12 or orig > 255 * (total - 12) + 16:
+        raise nat.NativeError(-1, "frame header inconsistent with the frame's size")
     out = ctypes.create_string_buffer(max(orig, 1))
     n = ctypes.c_int64()
     check(lib().pastar_wire_frame_decode(frame, len(frame), out, orig, ctypes.byref(n)))
@@ -456,9 +471,11 @@ class PriorityList:
         n = self.engine.n
         return [Node(tuple(out[k].pos[:n]), out[k].g, out[k].f, out[k].parent_mask) for k in range(cnt.value)]
 
-    def conditional_enqueue(self, nodes):
-        """PAStar::enqueue over a batch (the ClosedList check, then
-        PriorityList::conditional_enqueue): which nodes entered the OpenList."""
+    def enqueue(self, nodes):
+        """PAStar::enqueue (PAStar.cpp:219-237) over a batch: the ClosedList
+        check, then PriorityList::conditional_enqueue.  The reference returns
+        nothing; this returns which nodes are now the OpenList's record of
+        their coordinate."""
         nodes = list(nodes) if not isinstance(nodes, Node) else [nodes]
         if not nodes:
             return []
@@ -468,7 +485,15 @@ class PriorityList:
                                             ctypes.byref(reop)))
         return [bool(a) for a in added]
 
-    enqueue = conditional_enqueue
+    def conditional_enqueue(self, node):
+        """PriorityList::conditional_enqueue (PriorityList.h:104-113), with
+        the reference's return value: True whether the node was inserted,
+        replaced a worse record or was discarded as not better (:109-110
+        returns true for that too).  The ClosedList check of PAStar::enqueue
+        is part of the call (one device record serves both lists); every
+        call site of the reference makes that check first."""
+        self.enqueue([node])
+        return True
 
     def get_highest_priority(self):
         f = ctypes.c_int32()

@@ -25,7 +25,7 @@ def worker_loop(e):
     open_ = PriorityList(e)
     closed = ClosedList(e)
     goal = e.sequences.get_final_coord()
-    open_.conditional_enqueue([e.initial_node()])
+    open_.enqueue([e.initial_node()])
     expansions = 0
     while True:
         cur = open_.dequeue()
@@ -35,10 +35,10 @@ def worker_loop(e):
         if cur.pos == goal:
             if open_.get_highest_priority() < cur.f:
                 closed.erase(cur.pos)
-                open_.conditional_enqueue([cur])
+                assert open_.conditional_enqueue(cur) is True
                 continue
             return cur, expansions, open_, closed
-        open_.conditional_enqueue(e.get_neigh(cur)[0])
+        open_.enqueue(e.get_neigh(cur)[0])
 
 
 @pytest.mark.parametrize("name", ["test", "test2", "PF08184"])
@@ -89,28 +89,41 @@ def test_list_operations_semantics(kat):
         assert open_.dequeue() is None
         origin = e.initial_node()
         kids = e.get_neigh(origin)[0]
-        assert open_.conditional_enqueue(kids) == [True] * len(kids)
+        assert open_.enqueue(kids) == [True] * len(kids)
         assert open_.size() == len(kids)
         best = min(k.f for k in kids)
         assert open_.get_highest_priority() == best
-        # conditional_enqueue: an equal or larger f is discarded, a smaller
-        # one replaces the node's record
+        # conditional_enqueue returns true in all three of the reference's
+        # cases (PriorityList.h:104-113): an equal or larger f is discarded
+        # (:109-110 returns true), a smaller one replaces the node's record
         k0 = kids[0]
-        assert open_.conditional_enqueue([Node(k0.pos, k0.g + 5, k0.f + 5, k0.parenti)]) == [False]
-        assert open_.conditional_enqueue([Node(k0.pos, k0.g, k0.f, k0.parenti)]) == [False]
+        worse, same = Node(k0.pos, k0.g + 5, k0.f + 5, k0.parenti), Node(k0.pos, k0.g, k0.f, k0.parenti)
+        assert open_.conditional_enqueue(worse) is True and open_.find(k0.pos) == k0
+        assert open_.conditional_enqueue(same) is True and open_.find(k0.pos) == k0
+        assert open_.enqueue([worse, same]) == [False, False]
         lower = Node(k0.pos, k0.g - 7, k0.f - 7, k0.parenti)
-        assert open_.conditional_enqueue([lower]) == [True]
+        assert open_.conditional_enqueue(lower) is True
         assert open_.find(k0.pos) == lower and open_.size() == len(kids)
         # dequeue: lowest f first, into the ClosedList
         first = open_.dequeue()
         assert first.f == min(best, lower.f)
         assert closed.find(first.pos) == first and open_.find(first.pos) is None
         assert closed.size() == 1 and open_.size() == len(kids) - 1
-        # a closed node with a worse g is discarded, a better one reopens
-        assert open_.conditional_enqueue([first]) == [False]
+        # PAStar::enqueue: a closed node with a worse g is discarded, a better
+        # one leaves the ClosedList and is counted as reopened once
+        assert open_.enqueue([first]) == [False] and open_.reopened() == 0
         better = Node(first.pos, first.g - 1, first.f - 1, first.parenti)
-        assert open_.conditional_enqueue([better]) == [True]
+        assert open_.enqueue([better]) == [True]
         assert open_.reopened() == 1 and open_.find(first.pos) == better and closed.find(first.pos) is None
+        # ... and not again when the reopened node is dequeued
+        again = open_.dequeue()
+        assert again == better and closed.find(first.pos) == better
+        assert open_.reopened() == 1
+        # two improving entries of one batch reopen their node once
+        b1 = Node(first.pos, better.g - 2, better.f - 2, first.parenti)
+        b2 = Node(first.pos, better.g - 3, better.f - 3, first.parenti)
+        open_.enqueue([b1, b2])
+        assert open_.reopened() == 2 and open_.find(first.pos) == b2
         # ties: a batch of the lowest f
         t = open_.get_highest_priority()
         batch = open_.dequeue_batch(64)
