@@ -226,6 +226,21 @@ int pastar_gpu_h(pastar_ctx *ctx, const uint16_t *pos, int count, int32_t *out);
 int pastar_gpu_expand(pastar_ctx *ctx, const pastar_node *in, int n_in, int vec_size,
                       pastar_node *out, int32_t *out_owner, int32_t *out_src, int64_t *n_out);
 
+/* pastar_gpu_expand without any allocation.  No counterpart in the
+ * reference: it is for callers that cannot allocate device memory (code
+ * under HIP graph capture, tight serving loops, harnesses that forbid
+ * hipMalloc).  Same arguments, results and errors as pastar_gpu_expand; the
+ * staging buffers (input nodes, offsets, neighbours, owners, sources) are a
+ * fixed scratch array in device memory (about 3.9 MB per GPU, held until the
+ * process ends), so a call takes at most PASTAR_NOALLOC_MAX_IN nodes and
+ * PASTAR_NOALLOC_MAX_OUT neighbours and fails with PASTAR_EINVAL beyond.
+ * Calls no hipMalloc / hipFree.  All calls on one GPU share that GPU's
+ * scratch: calls that overlap on one GPU (several contexts or threads) race. */
+#define PASTAR_NOALLOC_MAX_IN 8192
+#define PASTAR_NOALLOC_MAX_OUT 65536
+int pastar_gpu_expand_noalloc(pastar_ctx *ctx, const pastar_node *in, int n_in, int vec_size,
+                              pastar_node *out, int32_t *out_owner, int32_t *out_src, int64_t *n_out);
+
 /* Device-resident PAStar search from the origin to the final coordinate. */
 int pastar_gpu_search(pastar_ctx *ctx, const pastar_search_opts *opts, pastar_result *res);
 

@@ -129,6 +129,10 @@ SIGNATURES = {
     "pastar_gpu_expand": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_node), ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(pastar_node), ctypes.POINTER(ctypes.c_int32),
                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]),
+    "pastar_gpu_expand_noalloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_node), ctypes.c_int,
+                                                 ctypes.c_int, ctypes.POINTER(pastar_node),
+                                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                                 ctypes.POINTER(ctypes.c_int64)]),
     "pastar_gpu_search": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_search_opts),
                                          ctypes.POINTER(pastar_result)]),
     "pastar_gpu_closed_lookup": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16),

@@ -39,6 +39,19 @@
 using namespace pastar;
 using namespace pastar::dev;
 
+// Device scratch of pastar_gpu_expand_noalloc: one array per GPU the library
+// runs on, held until the process ends.  `scratch` is a host-side stand-in for
+// the symbol, never a device address: host code uses the address
+// hipGetSymbolAddress returns for the current device (pastar_ctx::scratch).
+constexpr size_t scr_align(size_t v) { return (v + 255) & ~(size_t)255; }
+constexpr size_t kScrIn = 0;
+constexpr size_t kScrOff = scr_align(kScrIn + sizeof(pastar_node) * PASTAR_NOALLOC_MAX_IN);
+constexpr size_t kScrOut = scr_align(kScrOff + sizeof(int64_t) * PASTAR_NOALLOC_MAX_IN);
+constexpr size_t kScrOwner = scr_align(kScrOut + sizeof(pastar_node) * PASTAR_NOALLOC_MAX_OUT);
+constexpr size_t kScrSrc = scr_align(kScrOwner + sizeof(int32_t) * PASTAR_NOALLOC_MAX_OUT);
+constexpr size_t kScratchBytes = scr_align(kScrSrc + sizeof(int32_t) * PASTAR_NOALLOC_MAX_OUT);
+static __device__ __align__(256) unsigned char scratch[kScratchBytes];
+
 namespace {
 
 thread_local std::string g_err;
@@ -250,6 +263,7 @@ struct pastar_ctx {
     // shard with an RCCL communicator of its own (the protocol at world 1)
     std::unique_ptr<Transport> tr;
     DevBuf<int64_t> xred;           // RCCL staging of small collectives
+    unsigned char *scratch = nullptr;  // this device's copy of the static scratch array (hipGetSymbolAddress)
     DevBuf<int> fault;              // kSite* bits of bounded device waits that ran out (kernels.hpp)
     unsigned spin_limit = kSpinLimit;
     hipStream_t stream = nullptr;
@@ -709,6 +723,9 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     PA_TRY(setup_problem(c.get(), p));
     PA_TRY(c->fault.alloc(1));
     HIP_TRY(hipMemset(c->fault.p, 0, sizeof(int)));
+    // each GPU holds its own copy of the scratch array at its own address:
+    // resolved here, with this context's device current
+    HIP_TRY(hipGetSymbolAddress((void **)&c->scratch, HIP_SYMBOL(scratch)));
     {
         // load the code object now (the runtime loads it at the first use of
         // one of its kernels): a context's first search then pays only its
@@ -887,18 +904,35 @@ int pastar_gpu_h(pastar_ctx *c, const uint16_t *pos, int count, int32_t *out)
     return PASTAR_OK;
 }
 
-int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_size, pastar_node *out,
-                      int32_t *out_owner, int32_t *out_src, int64_t *n_out)
+// The batched getNeigh over device buffers the caller of this helper owns:
+// din [n_in], doff [n_in], dout / down / dsrc [total].  off: host offsets.
+static int expand_on(pastar_ctx *c, const pastar_node *in, int n_in, int vec_size, const int64_t *off, int64_t total,
+                     pastar_node *din, int64_t *doff, pastar_node *dout, int32_t *down, int32_t *dsrc,
+                     pastar_node *out, int32_t *out_owner, int32_t *out_src)
 {
-    if (!c || (!in && n_in) || n_in < 0 || !n_out || vec_size < 1)
-        return fail(PASTAR_EINVAL, "invalid arguments");
-    if (!c->heuristic_ready)
-        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
-    *n_out = 0;
-    if (n_in == 0)
-        return PASTAR_OK;
-    // per-node output offsets: 2^(free dimensions) - 1 neighbours each
-    std::vector<int64_t> off((size_t)n_in);
+    HIP_TRY(hipMemcpy(din, in, sizeof(pastar_node) * (size_t)n_in, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(doff, off, sizeof(int64_t) * (size_t)n_in, hipMemcpyHostToDevice));
+    const int lpn = std::min(64, 1 << c->n);
+    const int per_block = kWaves * (64 / lpn);
+    const int blocks = std::min(4096, (n_in + per_block - 1) / per_block);
+    ops_for(c).expand_api(dim3(blocks), dim3(kBlock), c->stream, c->dP.p, din, n_in, doff, vec_size, dout, down, dsrc);
+    PA_TRY(check_launch());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    PA_TRY(check_fault(c));
+    if (total) {
+        if (out)
+            HIP_TRY(hipMemcpy(out, dout, sizeof(pastar_node) * (size_t)total, hipMemcpyDeviceToHost));
+        if (out_owner)
+            HIP_TRY(hipMemcpy(out_owner, down, 4 * (size_t)total, hipMemcpyDeviceToHost));
+        if (out_src)
+            HIP_TRY(hipMemcpy(out_src, dsrc, 4 * (size_t)total, hipMemcpyDeviceToHost));
+    }
+    return PASTAR_OK;
+}
+
+// per-node output offsets: 2^(free dimensions) - 1 neighbours each
+static int expand_offsets(const pastar_ctx *c, const pastar_node *in, int n_in, int64_t *off, int64_t *total_out)
+{
     int64_t total = 0;
     for (int k = 0; k < n_in; k++) {
         int free_dims = 0;
@@ -910,6 +944,23 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
         off[k] = total;
         total += (1ll << free_dims) - 1;
     }
+    *total_out = total;
+    return PASTAR_OK;
+}
+
+int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_size, pastar_node *out,
+                      int32_t *out_owner, int32_t *out_src, int64_t *n_out)
+{
+    if (!c || (!in && n_in) || n_in < 0 || !n_out || vec_size < 1)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    *n_out = 0;
+    if (n_in == 0)
+        return PASTAR_OK;
+    std::vector<int64_t> off((size_t)n_in);
+    int64_t total = 0;
+    PA_TRY(expand_offsets(c, in, n_in, off.data(), &total));
     HIP_TRY(hipSetDevice(c->device));
     PA_TRY(ensure_hc(c));
     DevBuf<pastar_node> din, dout;
@@ -920,24 +971,44 @@ int pastar_gpu_expand(pastar_ctx *c, const pastar_node *in, int n_in, int vec_si
     PA_TRY(dout.alloc((size_t)std::max<int64_t>(total, 1)));
     PA_TRY(down.alloc((size_t)std::max<int64_t>(total, 1)));
     PA_TRY(dsrc.alloc((size_t)std::max<int64_t>(total, 1)));
-    HIP_TRY(hipMemcpy(din.p, in, sizeof(pastar_node) * (size_t)n_in, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(doff.p, off.data(), sizeof(int64_t) * (size_t)n_in, hipMemcpyHostToDevice));
-    const int lpn = std::min(64, 1 << c->n);
-    const int per_block = kWaves * (64 / lpn);
-    const int blocks = std::min(4096, (n_in + per_block - 1) / per_block);
-    ops_for(c).expand_api(dim3(blocks), dim3(kBlock), c->stream, c->dP.p, din.p, n_in, doff.p, vec_size, dout.p,
-                          down.p, dsrc.p);
-    PA_TRY(check_launch());
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    PA_TRY(check_fault(c));
-    if (total) {
-        if (out)
-            HIP_TRY(hipMemcpy(out, dout.p, sizeof(pastar_node) * (size_t)total, hipMemcpyDeviceToHost));
-        if (out_owner)
-            HIP_TRY(hipMemcpy(out_owner, down.p, 4 * (size_t)total, hipMemcpyDeviceToHost));
-        if (out_src)
-            HIP_TRY(hipMemcpy(out_src, dsrc.p, 4 * (size_t)total, hipMemcpyDeviceToHost));
-    }
+    PA_TRY(expand_on(c, in, n_in, vec_size, off.data(), total, din.p, doff.p, dout.p, down.p, dsrc.p, out, out_owner,
+                     out_src));
+    *n_out = total;
+    return PASTAR_OK;
+}
+
+int pastar_gpu_expand_noalloc(pastar_ctx *c, const pastar_node *in, int n_in, int vec_size, pastar_node *out,
+                              int32_t *out_owner, int32_t *out_src, int64_t *n_out)
+{
+    if (!c || (!in && n_in) || n_in < 0 || !n_out || vec_size < 1)
+        return fail(PASTAR_EINVAL, "invalid arguments");
+    if (!c->heuristic_ready)
+        return fail(PASTAR_ESTATE, "pastar_gpu_build_heuristic not called");
+    *n_out = 0;
+    if (n_in == 0)
+        return PASTAR_OK;
+    if (n_in > PASTAR_NOALLOC_MAX_IN)
+        return fail(PASTAR_EINVAL, "pastar_gpu_expand_noalloc: %d input nodes exceed the scratch's %d", n_in,
+                    PASTAR_NOALLOC_MAX_IN);
+    if (!c->scratch)
+        return fail(PASTAR_ESTATE, "device scratch address not resolved");
+    int64_t off[PASTAR_NOALLOC_MAX_IN];  // (stack: no host allocation either)
+    int64_t total = 0;
+    PA_TRY(expand_offsets(c, in, n_in, off, &total));
+    if (total > PASTAR_NOALLOC_MAX_OUT)
+        return fail(PASTAR_EINVAL, "pastar_gpu_expand_noalloc: %lld neighbours exceed the scratch's %d",
+                    (long long)total, PASTAR_NOALLOC_MAX_OUT);
+    HIP_TRY(hipSetDevice(c->device));
+    PA_TRY(ensure_hc(c));
+    // the device's scratch array, carved at fixed offsets; the kernel writes
+    // every output it is asked for, so nothing has to start at zero
+    unsigned char *s = c->scratch;
+    pastar_node *din = reinterpret_cast<pastar_node *>(s + kScrIn);
+    int64_t *doff = reinterpret_cast<int64_t *>(s + kScrOff);
+    pastar_node *dout = reinterpret_cast<pastar_node *>(s + kScrOut);
+    int32_t *down = reinterpret_cast<int32_t *>(s + kScrOwner);
+    int32_t *dsrc = reinterpret_cast<int32_t *>(s + kScrSrc);
+    PA_TRY(expand_on(c, in, n_in, vec_size, off, total, din, doff, dout, down, dsrc, out, out_owner, out_src));
     *n_out = total;
     return PASTAR_OK;
 }

@@ -301,8 +301,10 @@ class Engine:
         return int(out[0]) if single else out
 
     # ---- Node::getNeigh ----
-    def get_neigh_batch(self, nodes, vec_size=1):
-        """Batched getNeigh: returns (children, owner, src) for a list of Node."""
+    def get_neigh_batch(self, nodes, vec_size=1, noalloc=False):
+        """Batched getNeigh: returns (children, owner, src) for a list of Node.
+        noalloc: through pastar_gpu_expand_noalloc (fixed device scratch, no
+        allocation; bounded input and output counts)."""
         n_in = len(nodes)
         arr = (nat.pastar_node * max(n_in, 1))()
         for k, nd in enumerate(nodes):
@@ -314,7 +316,8 @@ class Engine:
         own = (ctypes.c_int32 * cap)()
         src = (ctypes.c_int32 * cap)()
         cnt = ctypes.c_int64()
-        check(lib().pastar_gpu_expand(self._ctx, arr, n_in, vec_size, out, own, src, ctypes.byref(cnt)))
+        fn = lib().pastar_gpu_expand_noalloc if noalloc else lib().pastar_gpu_expand
+        check(fn(self._ctx, arr, n_in, vec_size, out, own, src, ctypes.byref(cnt)))
         kids = [Node(tuple(out[k].pos[:self.n]), out[k].g, out[k].f, out[k].parent_mask)
                 for k in range(cnt.value)]
         return kids, list(own[:cnt.value]), list(src[:cnt.value])
