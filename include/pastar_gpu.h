@@ -41,7 +41,7 @@ extern "C" {
 #endif
 
 #define PASTAR_MAX_SEQ 16
-#define PASTAR_ABI_VERSION 2
+#define PASTAR_ABI_VERSION 3
 
 /* status codes */
 #define PASTAR_OK 0
@@ -121,6 +121,19 @@ typedef struct pastar_search_opts {
                                  depth - 1 more levels (0 = default, at most
                                  1024)                                     */
     int32_t mode;             /* PASTAR_MODE_*: which engine runs the search */
+    /* sharded search (n_shards > 1): the record exchange between shards    */
+    int32_t xchg_lag;         /* 0: a step's select sees the records the
+                                 shards sent in the step before (the exchange
+                                 sits between two steps); 1: the exchange and
+                                 the owner's insert of step i run beside the
+                                 expansion of step i + 1 (side stream), and
+                                 their records reach the select after        */
+    int32_t pad0;
+    int64_t xchg_block_records; /* most records one step carries to one shard
+                                 (the all-to-all's block, a power of two of
+                                 records sized per round from the demand seen,
+                                 from 4096 up to this; more wait in the
+                                 sender's ring); 0 = 2^20                    */
 } pastar_search_opts;
 
 /* pastar_search_opts.mode */
@@ -161,6 +174,12 @@ typedef struct pastar_result {
     int64_t solo;           /* 1 when the search ran on the LDS-resident path
                                (one launch: PairAlign, search, backtrace;
                                steps = levels, expand_ms = that launch)    */
+    /* sharded search */
+    int64_t xchg_backlog_steps; /* (step, destination) pairs whose records did
+                               not all fit the step's exchange block        */
+    int64_t xchg_backlog_max;   /* most records left waiting for one shard   */
+    int64_t host_waits;         /* times the host waited for the device during
+                               the step loop (one per round of steps)       */
 } pastar_result;
 
 typedef struct pastar_ctx pastar_ctx;

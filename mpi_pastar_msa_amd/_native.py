@@ -56,6 +56,9 @@ class pastar_search_opts(ctypes.Structure):
         ("eager", ctypes.c_int32),
         ("depth", ctypes.c_int32),
         ("mode", ctypes.c_int32),
+        ("xchg_lag", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
+        ("xchg_block_records", ctypes.c_int64),
     ]
 
 
@@ -83,6 +86,9 @@ class pastar_result(ctypes.Structure):
         ("select_ms", ctypes.c_double),
         ("gap_ms", ctypes.c_double),
         ("solo", ctypes.c_int64),
+        ("xchg_backlog_steps", ctypes.c_int64),
+        ("xchg_backlog_max", ctypes.c_int64),
+        ("host_waits", ctypes.c_int64),
     ]
 
     def as_dict(self):

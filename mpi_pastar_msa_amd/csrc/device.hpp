@@ -110,9 +110,8 @@ struct StepStats {
     unsigned long long row[kStatRows][2 * kStFields];  // one 128-B line per row
     unsigned long long ovf_near;  // chunk pool exhausted
     unsigned long long ovf_far;   // sub-queue chunk table exhausted
-    unsigned long long ovf_out;   // outbox capacity exceeded
+    unsigned long long ovf_out;   // outbox ring capacity exceeded
     unsigned long long pad;
-    unsigned long long outbox_count[8];
 };
 
 __device__ __forceinline__ unsigned long long *stat_row(StepStats *st, unsigned wave_global)
@@ -120,12 +119,74 @@ __device__ __forceinline__ unsigned long long *stat_row(StepStats *st, unsigned 
     return st->row[wave_global % kStatRows];
 }
 
-// Remote record sent to the owner shard over RCCL.
+// Remote record sent to the owner shard over RCCL.  flags bit 0: the sender
+// expands the node itself at this g (block-local continuation), so the owner
+// records it as closed at g instead of queueing it.
 template <int KW>
 struct Remote {
     uint64_t key[KW];
-    int32_t g, h, pmask, pad;
+    int32_t g, h, pmask, flags;
 };
+constexpr int kRecSenderExpands = 1;
+
+// ---------------------------------------------------------------------------
+// Shard exchange state (sharded search only).  Children owned by another
+// shard go to a ring per destination (positions are 64-bit counters: w
+// reserved by the expand kernel's appends, r consumed by the pack kernel).
+// Each step the pack kernel moves up to `block_recs` records per destination
+// from the ring into a fixed-size block {XHdr, records}; the blocks travel by
+// a fixed-size all-to-all (RCCL grouped send/recv, or peer reads in an
+// in-process shard group), so no count ever has to reach the host; what does
+// not fit stays in the ring for the next step (the header says how much).
+// The expand kernel runs on the main stream, pack / all-to-all / insert on
+// the side stream; per-step hand-over values live in kXSlots slots indexed
+// by step, because the main stream may run ahead of the side stream.
+// ---------------------------------------------------------------------------
+constexpr int kMaxShards = 8;
+constexpr int kXSlots = 4;
+// Every field but n is the same in all blocks a shard sends in one step, and
+// is computed from values that no longer change once the step's pack kernel
+// may run (StepInfo, the ring snapshot, the consumed positions): every shard
+// therefore folds the same G headers and takes the same decision.
+struct XHdr {
+    unsigned long long n;            // records in this block
+    unsigned long long sent_all;     // records the sender sends to all shards in this step
+    unsigned long long backlog_all;  // records still waiting in the sender's rings after this step
+    unsigned long long has_work;     // the sender's batch of this step was not empty
+    unsigned long long fail;         // kFail* bits / 0x100 step limit / 0x200 fault: the sender cannot go on
+    long long goal;                  // the sender's best goal g
+    unsigned long long step;         // (diagnostics)
+    unsigned long long low_b;        // low half: the sender's lowest live bucket (kBuckets: none); high
+                                     // half: most records it had for one destination in this step
+};
+static_assert(sizeof(XHdr) == 64, "block header");
+
+struct XState {
+    // ---- appended to by every expand wave (atomics): own line ----
+    alignas(128) unsigned long long w[kMaxShards];
+    // ---- published by pack, read by the expand kernel's overflow check ----
+    alignas(128) unsigned long long r_pub[kMaxShards];
+    // ---- per-step slots: the ring positions by the expand kernel's last
+    // block, the rest by the select kernel (one thread, once per step) ----
+    alignas(128) unsigned long long w_snap[kXSlots][kMaxShards];
+    struct StepInfo {
+        unsigned long long n_batch;
+        long long goal;
+        int fail, has_work, low_b, pad;
+    } info[kXSlots];
+    // lowest live bucket over all shards as of their last select (written by
+    // the insert kernel from the headers; kBuckets: none)
+    int gmin_b;
+    // ---- side stream only (pack / insert) ----
+    unsigned long long r[2][kMaxShards];  // consumed positions, by step parity
+    unsigned long long sent, received, sent_steps, backlog_max, backlog_steps;
+    unsigned long long demand_max;  // most records one shard had for one destination in a step, since the host's last reset
+    unsigned long long claimed_b, dropped_b;  // insert's table claims, folded by pack
+    int fail_b, fault_b;
+    int quiet_run;  // consecutive steps in which no shard had work, records or backlog
+    int pad0;
+};
+
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -455,6 +455,8 @@ struct Ctl {
     int fuse;       // 1: the last expand block also runs select for the next step
     int fail_mask;  // kFail* bits of the capacity that ran out
     int has_work;   // select found a live bucket (multi-shard termination)
+    int low_found;  // that bucket (kBuckets: none)
+    int xwindow;    // sharded: buckets above the shards' common lowest live bucket a batch may be cut from
     int debug;      // 1: select validates its scan start (diagnostics)
     int deep_blocks;  // block-rounds per continuation level across the chip (kDeepBlocks by default)
     unsigned long long kmax;
@@ -469,6 +471,11 @@ struct Ctl {
     // ---- atomics, one line each ----
     alignas(128) unsigned long long pool_top;  // chunk bump allocator
     alignas(128) int cur_b;  // lowest bucket that may hold entries (f_min only grows)
+    // lowest bucket appended to by kernels that run beside select (the sharded
+    // search's insert kernel on the side stream): select takes it by exchange
+    // and starts its scan there, so a lowering can never be lost under
+    // select's own store of cur_b (kBuckets: none)
+    alignas(128) int low_b;
     // arrival counters of the expand blocks (two levels: blockIdx % kArrive,
     // then the groups), reset by the last block
     alignas(128) unsigned arrive_top;
@@ -536,8 +543,12 @@ struct SearchArgs {
     Entry *pool;          // [pool_chunks][kChunk]
     StepStats *stats;
     int *goal_g;
-    void *outbox;  // Remote<KW>[n_shards][outbox_cap]
-    unsigned long long outbox_cap;
+    void *outbox;  // Remote<KW>[n_shards][outbox_cap]: a ring per destination shard
+    unsigned long long outbox_cap;  // a power of two
+    int *lower;    // the word an append below the lowest bucket in use lowers: Ctl::cur_b, or Ctl::low_b
+                   // for appends that run beside a select (the sharded search's insert kernel)
+    XState *x;     // shard exchange state (nullptr: one-shard search)
+    int step;      // this launch's step (its slot of XState's per-step values)
     // the open-list capacities (= Ctl's), as kernel arguments: an append
     // then computes its chunk-table address without a load of the control
     // block ahead of the chunk-table read
@@ -558,6 +569,35 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v)
     for (int o = 32; o > 0; o >>= 1)
         v += __shfl_xor(v, o);
     return v;
+}
+
+// Wave-aggregated append to a destination's outbox ring: one atomic per wave
+// on the ring's append position; a record that would overrun what the pack
+// kernel has consumed (r, read possibly stale, i.e. low: conservative) is
+// counted as an outbox overflow.  Must be reached by every lane of the wave.
+template <typename T>
+__device__ __forceinline__ void ring_append(bool pred, unsigned long long *w, const unsigned long long *r_pub, T *ring,
+                                            unsigned long long cap, const T &v, unsigned long long *overflow)
+{
+    const uint64_t mask = __ballot(pred);
+    if (!mask)
+        return;
+    const int lane = lane_id();
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned long long base = 0, r = 0;
+    if (lane == leader) {
+        base = atomicAdd(w, (unsigned long long)__popcll(mask));
+        r = __hip_atomic_load(r_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    base = bcast_lane(base, leader);
+    r = bcast_lane(r, leader);
+    if (pred) {
+        const unsigned long long pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+        if (pos - r < cap)
+            ring[pos & (cap - 1)] = v;
+        else
+            atomicAdd(overflow, 1ull);
+    }
 }
 
 // Loads of words other blocks of the same launch update with atomics (the
@@ -656,9 +696,14 @@ __device__ __forceinline__ void queue_append(const SearchArgs &a, bool pred, int
         unsigned long long base = 0;
         if (lane == leader) {
             base = queue_reserve(a, bl, sq, (unsigned)__popcll(m));
-            // entries from other shards may land below this shard's minimum
-            if (may_lower && bl < ld_agent(&a.ctl->cur_b))
-                atomicMin(&a.ctl->cur_b, bl);
+            // entries from other shards may land below this shard's minimum:
+            // lowered after the cursor add has returned (the reservation is
+            // performed before whoever sees the lowered word reads the cursor)
+            if (may_lower) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (bl < ld_agent(a.lower))
+                    atomicMin(a.lower, bl);
+            }
 #ifdef PASTAR_TRACE_APPENDS
             if (a.trace) {
                 const long long stp = ld_agent(&a.ctl->steps);
@@ -729,7 +774,15 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
 {
     bool improved = false, cl = false;
     int64_t slot = 0;
-    if (valid && local) {
+    // Sharded search: a child owned by another shard is relaxed into this
+    // shard's table too (a record of the best g this shard has sent for it)
+    // and goes to its owner only when that improved: each shard sends a
+    // node once per improvement it finds, not once per parent, which cuts
+    // the exchange by the number of parents a shard holds of one node.  The
+    // owner's table alone is authoritative for the node (open list,
+    // closed mark, backtrace).
+    const bool filter = SH && P.n_shards > 1;
+    if (valid && (local || filter)) {
         slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre);
         if (slot < 0) {
             if (slot == -2)
@@ -749,9 +802,9 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
     }
     const int f = g + h;
     const Entry e = {(uint32_t)slot, f};
-    bool global = improved;
+    bool global = improved && local;
     if (lp.buf) {
-        const bool want = improved && f < lp.f_limit;
+        const bool want = improved && local && f < lp.f_limit;
         const uint64_t mask = __ballot(want);
         if (mask) {
             const int lane = lane_id();
@@ -797,7 +850,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
     }
     queue_append(a, global, bucket_of(f, f0, w), e, st, remote_in);
     if (SH && P.n_shards > 1) {
-        const bool remote = valid && !local;
+        const bool remote = valid && !local && improved;
         Remote<KW> rec;
 #pragma unroll
         for (int k = 0; k < KW; k++)
@@ -805,10 +858,10 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
         rec.g = g;
         rec.h = h;
         rec.pmask = m;
-        rec.pad = 0;
+        rec.flags = 0;
         Remote<KW> *ob = (Remote<KW> *)a.outbox;
         for (int d = 0; d < P.n_shards; d++)
-            wave_append(remote && owner == d, &st->outbox_count[d], ob + (size_t)d * a.outbox_cap, a.outbox_cap,
+            ring_append(remote && owner == d, &a.x->w[d], &a.x->r_pub[d], ob + (size_t)d * a.outbox_cap, a.outbox_cap,
                         rec, &st->ovf_out);
     }
 }
@@ -854,7 +907,8 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     static_assert(kStatRows == 64, "one wave sums the stat rows");
     static_assert(kWin >= kWide, "the first window covers a batch's buckets");
     static_assert(kRanges == 128 && kSub % 2 == 0, "one wave cuts the batch, two ranges per lane");
-    __shared__ int found, found2, goal_s, cur_s, fail_s, fault_s;
+    __shared__ int found, found2, goal_s, cur_s, fail_s, fault_s, low_s, gmin_s;
+    __shared__ unsigned long long claimed_b_s;
     __shared__ unsigned long long wv[kBlock], rv[kBlock];
     __shared__ unsigned long long sums[kStFields], ovf[3];
     const bool prof = v.timing & 2;
@@ -913,6 +967,10 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         found2 = kBuckets;
     } else if (tid == kStatRows + 6) {
         fault_s = ld_agent(a.fault);
+    } else if (tid == kStatRows + 7) {
+        low_s = ld_agent(&ctl->low_b) < kBuckets ? atomicExch(&ctl->low_b, kBuckets) : kBuckets;
+        claimed_b_s = a.x ? a.x->claimed_b : 0;
+        gmin_s = a.x ? ld_agent(&a.x->gmin_b) : kBuckets;
     }
     __syncthreads();
     PHASE(0)
@@ -925,10 +983,10 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         ctl->dropped = acc[4] + sums[kStDropped];
         ctl->parents = acc[5] + v.n_batch;
         int fm = fail_bits(ovf[0], ovf[1], sums[kStOvfTable], ovf[2]);
-        if (claimed * 10 > v.table_slots * 7)
+        if ((claimed + claimed_b_s) * 10 > v.table_slots * 7)
             fm |= kFailTable;
         if (fm) {
-            ctl->fail_mask |= fm;
+            atomicOr(&ctl->fail_mask, fm);
             ctl->status = 2;
         }
         if (fault_s) {  // a bounded device wait ran out: the search's state is no longer exact
@@ -939,7 +997,17 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     }
     const int goal = goal_s;
     const int limit = goal == kIntMax ? kBuckets - 1 : bucket_of(goal, f0, w);
-    const int start = cur_s < b_win ? cur_s : b_win;
+    // Sharded search: a batch is cut only from the kWide buckets above the
+    // lowest live bucket of ALL shards (as of their last select; every
+    // shard's header carries its own).  A shard whose own buckets lie higher
+    // waits: what it would expand from them now, it would mostly expand
+    // again once the cheaper paths through the other shards' lower buckets
+    // arrive (syn8x400 at 8 shards: 27-46 M expansions for 5.8 M without
+    // the window).  limit still decides whether the shard has work at all.
+    const int xwin = ctl->xwindow;
+    const int limit_take = (gmin_s < kBuckets && gmin_s + xwin - 1 < limit) ? gmin_s + xwin - 1 : limit;
+    const int start_c = cur_s < b_win ? cur_s : b_win;
+    const int start = low_s < start_c ? low_s : start_c;
     if (start == b_win) {
         const int bb = b_win + tid / kSub;
         if (bb <= limit && wv[tid] > rv[tid])
@@ -998,10 +1066,25 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
             t[5] = b;
         }
     }
+    if (b < kBuckets && b > limit_take) {
+        // live entries, but above the shards' common window: an idle step
+        if (tid == 0) {
+            ctl->n_batch = 0;
+            ctl->has_work = 1;
+            ctl->low_found = b;
+            st_agent(&ctl->cur_b, b);
+            const long long steps = ctl->steps + 1;
+            ctl->steps = steps;
+            if (ctl->max_steps && steps >= ctl->max_steps)
+                ctl->status = 3;
+        }
+        return;
+    }
     if (b >= kBuckets) {
         if (tid == 0) {
             ctl->n_batch = 0;
             ctl->has_work = 0;
+            ctl->low_found = kBuckets;
             const long long steps = ctl->steps + 1;
             ctl->steps = steps;
             // one shard: done; the sharded protocol decides on the host
@@ -1027,7 +1110,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         for (int j = 0; j < 2; j++) {
             const int r = 2 * tid + j;
             const int bb = b + r / kSub, sq = r % kSub;
-            const bool in = bb <= limit && bb < kBuckets;
+            const bool in = bb <= limit_take && bb < kBuckets;
             unsigned long long rsv = 0, wr = 0;
             if (in) {
                 if (start == b_win && bb < b_win + kWin) {
@@ -1053,9 +1136,29 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         const unsigned long long ex0 = inc - s2, ex1 = ex0 + av[0];
         const int k = (2 * tid) / kSub;                       // bucket offset of both ranges
         const unsigned long long bstart = __shfl(ex0, k * (kSub / 2));  // entries before bucket k
-        const bool incl = k == 0 || bstart < v.kmin;
-        const int n_incl = __popcll(__ballot(incl && (tid % (kSub / 2)) == 0 && b + k <= limit));
-        const unsigned long long kmax = v.kmax;
+        // (sharded: a shard holds about 1 / n_shards of a thin bucket)
+        const unsigned long long kmin = a.x ? v.kmin / (unsigned long long)ctl->n_shards : v.kmin;
+        const bool incl = k == 0 || bstart < kmin;
+        const int n_incl = __popcll(__ballot(incl && (tid % (kSub / 2)) == 0 && b + k <= limit_take));
+        // sharded: no more parents than the outbox rings can take children
+        // of (a ring holds what the exchange has not carried off yet): the
+        // least free ring, spread over the other shards, at half the masks
+        // a parent can have (an overflow past this estimate restarts the
+        // search with larger rings)
+        unsigned long long kmax = v.kmax;
+        if (a.x && ctl->n_shards > 1) {
+            unsigned long long free_min = ~0ull;
+            for (int d = 0; d < ctl->n_shards; d++) {
+                if (d == a.P->shard)
+                    continue;
+                const unsigned long long used = ld_agent(&a.x->w[d]) - ld_agent(&a.x->r_pub[d]);
+                const unsigned long long fr = used < a.outbox_cap ? a.outbox_cap - used : 0;
+                free_min = fr < free_min ? fr : free_min;
+            }
+            const unsigned long long masks = (1ull << a.P->n) - 1;
+            const unsigned long long lim = free_min * (unsigned long long)(ctl->n_shards - 1) * 2 / masks;
+            kmax = lim < kmax ? lim : kmax;
+        }
         const unsigned long long t0 = incl ? (ex0 < kmax ? (av[0] < kmax - ex0 ? av[0] : kmax - ex0) : 0) : 0;
         const unsigned long long t1 = incl ? (ex1 < kmax ? (av[1] < kmax - ex1 ? av[1] : kmax - ex1) : 0) : 0;
         const unsigned long long total = wave_sum(t0 + t1);
@@ -1077,6 +1180,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
             ctl->batch_nb = n_incl > 0 ? n_incl : 1;
             st_agent(&ctl->cur_b, b);
             ctl->has_work = 1;
+            ctl->low_found = b;
             const long long steps = ctl->steps + 1;
             ctl->steps = steps;
             if (ctl->max_steps && steps >= ctl->max_steps)
@@ -1089,9 +1193,37 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
 
 __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
 {
-    if (a.ctl->status)
+    if (!a.ctl->status)
+        select_block(a, load_view(a.ctl));
+    if (!a.x)
         return;
-    select_block(a, load_view(a.ctl));
+    // Sharded search: what this shard tells the others about step a.step,
+    // sampled here once, by one thread, before the step's expansion: the
+    // pack kernel copies it into every block header, whatever else changes
+    // meanwhile (the side stream may set the status, the next step's select
+    // may run beside the pack).
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const Ctl *ctl = a.ctl;
+        const int status = ld_agent(&ctl->status);
+        XState::StepInfo si;
+        si.n_batch = status == 0 ? ctl->n_batch : 0;
+        si.has_work = status == 0 && ctl->has_work;
+        si.low_b = si.has_work ? ctl->low_found : kBuckets;
+        si.goal = ld_agent(a.goal_g);
+        int fl = 0;
+        if (status == 2)
+            fl |= ctl->fail_mask & 0xff ? ctl->fail_mask & 0xff : kFailTable;
+        else if (status == 3)
+            fl |= 0x100;
+        else if (status == 4)
+            fl |= 0x200;
+        fl |= ld_agent(&a.x->fail_b);  // the insert kernel's overflows (folded by the pack kernel)
+        if (ld_agent(a.fault))
+            fl |= 0x200;
+        si.fail = fl;
+        a.x->info[a.step & (kXSlots - 1)] = si;
+    }
 }
 
 // A batch parent's slot words: key, best, aux.
@@ -1741,7 +1873,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
 #endif
 #undef BLK_COUNT
     const bool fuse = ctl->fuse;
-    if (!fuse && !timing)
+    const bool xsnap = SH && a.x != nullptr;  // sharded: the last block publishes the step's hand-over values
+    if (!fuse && !timing && !xsnap)
         return;
     // the last block to finish: two-level arrival (blockIdx % kArrive, then
     // the groups) so that no counter takes more than ~64 arrivals
@@ -1780,6 +1913,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         st_agent(&ctl->arrive[threadIdx.x], 0u);
     if (threadIdx.x == 0)
         st_agent(&ctl->arrive_top, 0u);
+    if (xsnap) {
+        // every block's ring appends are complete (each wave waited for its
+        // own before arriving): the positions reserved so far are what the
+        // pack kernel of this step may take
+        const int slot = a.step & (kXSlots - 1);
+        if (threadIdx.x < kMaxShards)
+            st_agent(&a.x->w_snap[slot][threadIdx.x], ld_agent(&a.x->w[threadIdx.x]));
+    }
     unsigned long long t0 = 0;
     if (timing) {
         __shared__ unsigned long long t_lo;
@@ -1839,8 +1980,8 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
             m = r.pmask;
             valid = g + h < bound;
         }
-        route_child<KW>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf, LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr},
-                        true);
+        route_child<KW, 1, false>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf,
+                                  LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr}, true);
     }
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);
@@ -1853,22 +1994,253 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     }
 }
 
-// The values a shard publishes after its step (sharded search), packed on
-// the device so that the gather of every shard's values is the step's only
-// host round trip: records for each shard (own: 0), goal g, had work, failed.
-__global__ void step_pack_kernel(SearchArgs a, unsigned long long outbox_cap, int64_t *__restrict__ out)
+// ---------------------------------------------------------------------------
+// Shard exchange kernels (side stream).  One step:
+//   xpack    ring -> fixed-size blocks, one per destination shard, each with
+//            a header {records, backlog, had work, failed, goal}
+//   (all-to-all of the blocks: RCCL send/recv, or xcopy in a shard group)
+//   xinsert  relax the received records on their owner; fold the headers:
+//            the best goal, failures, and the termination count
+// They replace the reference's sender / receiver / message processor threads
+// (PAStarSender.cpp:10-131, PAStarReceiver.cpp:11-120,
+// PAStarMessageProcesser.cpp:12-78) and check_stop's allreduces
+// (PAStar.cpp:502-519).
+// ---------------------------------------------------------------------------
+struct XArgs {
+    XState *x;
+    Ctl *ctl;
+    StepStats *stats_b;  // the insert kernel's own step statistics
+    const int *goal_g;
+    const int *fault;
+    void *outbox;        // Remote<KW>[n_shards][outbox_cap] rings
+    unsigned long long outbox_cap;
+    unsigned char *send;  // [n_shards] blocks of block_bytes
+    unsigned char *recv;  // [n_shards] blocks of block_bytes
+    unsigned long long block_bytes, block_recs;
+    int n_shards, shard, step, lag;
+};
+
+__device__ __forceinline__ XHdr *xblock_hdr(unsigned char *blocks, unsigned long long block_bytes, int d)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0)
-        return;
-    const Ctl *ctl = a.ctl;
-    const int G = ctl->n_shards, me = a.P->shard;
-    for (int d = 0; d < G; d++) {
-        const unsigned long long k = a.stats->outbox_count[d];
-        out[d] = d == me ? 0 : (int64_t)(k < outbox_cap ? k : outbox_cap);
+    return reinterpret_cast<XHdr *>(blocks + (size_t)d * block_bytes);
+}
+
+// grid (n_shards, blocks per destination)
+template <int KW>
+__global__ __launch_bounds__(kBlock) void xpack_kernel(XArgs t)
+{
+    XState *x = t.x;
+    const int d = blockIdx.x, par = t.step & 1, slot = t.step & (kXSlots - 1);
+    // fold the insert kernel's statistics of the step before (stream order:
+    // that launch is complete, the next one not started)
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+        StepStats *sb = t.stats_b;
+        if (threadIdx.x < kStatRows) {
+            unsigned long long cl = sb->row[threadIdx.x][kStClaimed], ov = sb->row[threadIdx.x][kStOvfTable];
+            sb->row[threadIdx.x][kStClaimed] = 0;
+            sb->row[threadIdx.x][kStOvfTable] = 0;
+            cl = wave_sum(cl);
+            ov = wave_sum(ov);
+            if (threadIdx.x == 0) {
+                x->claimed_b += cl;
+                const int fm = fail_bits(sb->ovf_near, sb->ovf_far, ov, sb->ovf_out);
+                sb->ovf_near = sb->ovf_far = sb->ovf_out = 0;
+                if (fm)
+                    atomicOr(&x->fail_b, fm);  // read by the next select (StepInfo::fail)
+            }
+        }
     }
-    out[G] = *a.goal_g;
-    out[G + 1] = ctl->has_work;
-    out[G + 2] = ctl->status >= 2 ? 1 : 0;  // capacity exhausted or step limit
+    __syncthreads();
+    // this step's share of every destination's ring, from values that are
+    // fixed by now: the ring positions the expand kernel's last block
+    // published (a launch that left early publishes nothing: the slot then
+    // holds an older, lower position, which only sends less), the positions
+    // the last pack consumed, and the select kernel's StepInfo
+    const XState::StepInfo si = x->info[slot];
+    const bool stopped = si.fail != 0;
+    unsigned long long r0 = 0, n = 0, sent_all = 0, backlog_all = 0, pair_max = 0;
+    for (int k = 0; k < t.n_shards; k++) {
+        const unsigned long long rk = x->r[par][k], wk = ld_agent(&x->w_snap[slot][k]);
+        const unsigned long long avail = (k == t.shard || stopped || wk < rk) ? 0 : wk - rk;
+        const unsigned long long nk = avail < t.block_recs ? avail : t.block_recs;
+        sent_all += nk;
+        backlog_all += avail - nk;
+        pair_max = avail > pair_max ? avail : pair_max;
+        if (k == d) {
+            r0 = rk;
+            n = nk;
+        }
+    }
+    const Remote<KW> *ring = reinterpret_cast<const Remote<KW> *>(t.outbox) + (size_t)d * t.outbox_cap;
+    Remote<KW> *dst = reinterpret_cast<Remote<KW> *>(t.send + (size_t)d * t.block_bytes + sizeof(XHdr));
+    for (unsigned long long k = (unsigned long long)blockIdx.y * blockDim.x + threadIdx.x; k < n;
+         k += (unsigned long long)gridDim.y * blockDim.x)
+        dst[k] = ring[(r0 + k) & (t.outbox_cap - 1)];
+    if (blockIdx.y == 0 && threadIdx.x == 0) {
+        x->r[par ^ 1][d] = r0 + n;
+        st_agent(&x->r_pub[d], r0 + n);
+        XHdr h{};
+        h.n = n;
+        h.sent_all = sent_all;
+        h.backlog_all = backlog_all;
+        h.has_work = si.has_work != 0;
+        h.low_b = (unsigned long long)(unsigned)si.low_b | (pair_max << 32);
+        h.fail = (unsigned long long)si.fail;
+        h.goal = si.goal;
+        h.step = (unsigned long long)t.step;
+        *xblock_hdr(t.send, t.block_bytes, d) = h;
+        if (d == t.shard) {  // this shard's own header needs no transport
+            *xblock_hdr(t.recv, t.block_bytes, d) = h;
+            x->sent += sent_all;
+            if (backlog_all) {
+                x->backlog_steps++;
+                if (backlog_all > x->backlog_max)
+                    x->backlog_max = backlog_all;
+            }
+        }
+    }
+}
+
+// In-process shard group: block s of this shard's inbox is read from shard
+// s's send area (src[s] points at the block shard s packed for this shard).
+// grid (n_shards, blocks per source)
+struct XPeers {
+    const unsigned char *src[kMaxShards];
+};
+
+__global__ __launch_bounds__(kBlock) void xcopy_kernel(XPeers p, unsigned char *recv, unsigned long long block_bytes,
+                                                       unsigned long long rec_bytes, int shard)
+{
+    const int s = blockIdx.x;
+    if (s == shard)
+        return;
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 *src = reinterpret_cast<const u64x2 *>(p.src[s]);
+    u64x2 *dst = reinterpret_cast<u64x2 *>(recv + (size_t)s * block_bytes);
+    unsigned long long n = reinterpret_cast<const XHdr *>(src)->n;
+    const unsigned long long fit = (block_bytes - sizeof(XHdr)) / rec_bytes;
+    n = n < fit ? n : fit;  // (never past the block, whatever the header says)
+    const unsigned long long vecs = (sizeof(XHdr) + n * rec_bytes + 15) / 16;
+    for (unsigned long long k = (unsigned long long)blockIdx.y * blockDim.x + threadIdx.x; k < vecs;
+         k += (unsigned long long)gridDim.y * blockDim.x)
+        dst[k] = src[k];
+}
+
+// Relax the records received from the other shards (the owner side of the
+// exchange; replaces PAStarMessageProcesser -> enqueue, PAStar.cpp:241-250),
+// and fold every shard's header: the best goal, failures, and termination
+// (check_stop, PAStar.cpp:480-547): the search ends when, for lag + 1 steps
+// in a row, no shard had a batch, sent a record or kept a backlog; every
+// shard sees the same headers and so decides the same at the same step.
+template <int KW>
+__global__ __launch_bounds__(kBlock) void xinsert_kernel(SearchArgs a, XArgs t)
+{
+    const DevProblem &P = *a.P;
+    Ctl *ctl = a.ctl;
+    StepStats *st = a.stats;  // the side stream's own statistics (XArgs::stats_b)
+    const int G = t.n_shards;
+    __shared__ unsigned long long pre[kMaxShards + 1];
+    __shared__ int goal_s;
+    if (threadIdx.x == 0) {
+        unsigned long long tot = 0, backlog = 0, demand = 0;
+        int work = 0, fl = 0, gmin = kBuckets;
+        long long goal = kIntMax;
+        for (int s = 0; s < G; s++) {
+            const XHdr *h = xblock_hdr(t.recv, t.block_bytes, s);
+            pre[s] = tot;
+            const unsigned long long n = s == t.shard ? 0 : (h->n <= t.block_recs ? h->n : t.block_recs);
+            tot += n;
+            // (only fields that are the same in every block of sender s)
+            backlog += h->backlog_all;
+            work |= h->has_work != 0 || h->sent_all != 0;
+            // the most one shard had for one destination in a step (sent and
+            // left over): sizes the next round's blocks, the same on every shard
+            if ((h->low_b >> 32) > demand)
+                demand = h->low_b >> 32;
+            if ((int)(unsigned)h->low_b < gmin)
+                gmin = (int)(unsigned)h->low_b;
+            fl |= (int)h->fail;
+            if (h->goal < goal)
+                goal = h->goal;
+        }
+        pre[G] = tot;
+        goal_s = (int)goal;
+        if (blockIdx.x == 0) {
+            XState *x = t.x;
+            x->received += tot;
+            if (demand > x->demand_max)
+                x->demand_max = demand;
+            st_agent(&x->gmin_b, gmin);
+            if (goal < ld_agent(a.goal_g))
+                atomicMin(a.goal_g, (int)goal);
+            const int status = ld_agent(&ctl->status);
+            if (fl && status < 2) {
+                // a shard failed: every shard stops at this step (each
+                // reports its own fail bits; 0x200: a device wait ran out)
+                if (fl & 0x200) {
+                    ctl->fault_sites = *t.fault;
+                    ctl->status = 4;
+                } else if (fl & 0x100) {
+                    ctl->status = 3;
+                } else {
+                    atomicOr(&ctl->fail_mask, x->fail_b | 0x1000);  // 0x1000: some shard ran out of capacity
+                    ctl->status = 2;
+                }
+            } else if (status == 0) {
+                const bool quiet = !work && backlog == 0;
+                const int run = quiet ? x->quiet_run + 1 : 0;
+                x->quiet_run = run;
+                if (run > t.lag)
+                    ctl->status = 1;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned long long count = pre[G];
+    if (count == 0)
+        return;
+    const int w = ctl->band_log2, f0 = ctl->f0;
+    int bound = *(volatile int *)a.goal_g;
+    if (goal_s < bound)
+        bound = goal_s;
+    unsigned claimed = 0, ovf = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    const unsigned long long iters = (count + stride - 1) / stride;
+    for (unsigned long long it = 0; it < iters; it++) {
+        const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x + it * stride;
+        bool valid = i < count;
+        uint64_t ck[KW];
+        int g = 0, h = 0, m = 0;
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            ck[k] = 0;
+        if (valid) {
+            int s = 0;
+            while (pre[s + 1] <= i)
+                s++;
+            const Remote<KW> *recs =
+                reinterpret_cast<const Remote<KW> *>(t.recv + (size_t)s * t.block_bytes + sizeof(XHdr));
+            const Remote<KW> r = recs[i - pre[s]];
+#pragma unroll
+            for (int k = 0; k < KW; k++)
+                ck[k] = r.key[k];
+            g = r.g;
+            h = r.h;
+            m = r.pmask;
+            valid = g + h < bound;
+        }
+        route_child<KW, 1, false>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf,
+                                  LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr}, true);
+    }
+    claimed = wave_sum(claimed);
+    ovf = wave_sum(ovf);
+    if (lane_id() == 0) {
+        unsigned long long *row = stat_row(st, (blockIdx.x * blockDim.x + threadIdx.x) / 64);
+        if (claimed)
+            atomicAdd(&row[kStClaimed], (unsigned long long)claimed);
+        if (ovf)
+            atomicAdd(&row[kStOvfTable], (unsigned long long)ovf);
+    }
 }
 
 // Reset the open list between searches: zero the chunk-table entries the

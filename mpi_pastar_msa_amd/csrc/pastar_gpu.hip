@@ -136,18 +136,21 @@ struct Transport {
     virtual ~Transport() = default;
     // element-wise reduction of host int64 values over all shards
     virtual int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) = 0;
-    // outbox segment d -> inbox of shard d at that shard's roff[me]
-    virtual int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
-                                 const unsigned long long *roff, size_t rb, size_t outbox_cap) = 0;
     // device buffer of `root` copied to every shard's same buffer
     virtual int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) = 0;
-    // every shard's `count` device values (dev_mine, written by earlier work
-    // on the context's stream), concatenated in shard order into the host
-    // array all[G * count] (count <= kGatherMax); returns with the stream
-    // drained, so it is the caller's one host round trip
-    virtual int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) = 0;
+    // once per search, after the exchange buffers are allocated (collective)
+    virtual int xchg_setup(pastar_ctx *c) = 0;
+    // one step's all-to-all of the fixed-size blocks, enqueued on the side
+    // stream behind the step's pack kernel: block d of this shard's send
+    // area (parity step & 1) becomes block `shard` of shard d's receive area.
+    // Nothing here waits for the device.
+    virtual int xchg(pastar_ctx *c, int step) = 0;
+    // this shard cannot go on: release the shards that wait for it on the
+    // host, where the transport can (an in-process group; RCCL peers are
+    // left to their own time limits, as MPI ranks are)
+    virtual void abort() {}
 };
-constexpr int kGatherMax = 16;
+constexpr int kEvRing = 8;  // events per stream hand-over, reused round-robin by step
 
 }  // namespace
 
@@ -160,7 +163,8 @@ struct pastar_group {
     bool broken = false;
     std::vector<std::array<int64_t, 16>> vals;
     std::vector<std::vector<unsigned long long>> counts;
-    std::vector<const uint8_t *> outbox;
+    std::vector<std::array<const unsigned char *, 2>> xsend;  // each shard's send areas, by parity
+    std::vector<std::array<hipEvent_t, kEvRing>> ev_pack;     // each shard's "blocks packed" events
     std::vector<void *> bufs;
     std::vector<int> device;
     std::atomic<int> members{0};
@@ -221,20 +225,10 @@ class LocalTransport : public Transport {
         }
         return sync();
     }
-    int exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
-                         const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
-    int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) override;
-    int allgather(const int64_t *mine, int count, int64_t *all)
-    {
-        for (int k = 0; k < count; k++)
-            g_->vals[rank_][k] = mine[k];
-        PA_TRY(sync());
-        for (int s2 = 0; s2 < g_->G; s2++)
-            for (int k = 0; k < count; k++)
-                all[s2 * count + k] = g_->vals[s2][k];
-        return sync();
-    }
+    int xchg_setup(pastar_ctx *c) override;
+    int xchg(pastar_ctx *c, int step) override;
+    void abort() override { g_->breakdown(); }
 
    private:
     pastar_group *g_;
@@ -243,16 +237,24 @@ class LocalTransport : public Transport {
 
 class RcclTransport : public Transport {
    public:
-    explicit RcclTransport(ncclComm_t comm) : comm_(comm) {}
-    ~RcclTransport() override { ncclCommDestroy(comm_); }
+    // xcomm: the record exchange's own communicator (ncclCommSplit of comm),
+    // so that the side stream's send/recv and the main stream's collectives
+    // are never ordered against each other on one communicator; nullptr
+    // when the split is unavailable (everything then runs on comm)
+    RcclTransport(ncclComm_t comm, ncclComm_t xcomm) : comm_(comm), xcomm_(xcomm) {}
+    ~RcclTransport() override
+    {
+        if (xcomm_)
+            ncclCommDestroy(xcomm_);
+        ncclCommDestroy(comm_);
+    }
     int allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op) override;
-    int exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
-                         const unsigned long long *roff, size_t rb, size_t outbox_cap) override;
     int broadcast(pastar_ctx *c, void *dev, size_t bytes, int root) override;
-    int gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all) override;
+    int xchg_setup(pastar_ctx *) override { return PASTAR_OK; }
+    int xchg(pastar_ctx *c, int step) override;
 
    private:
-    ncclComm_t comm_;
+    ncclComm_t comm_, xcomm_;
 };
 
 }  // namespace
@@ -268,6 +270,17 @@ struct pastar_ctx {
     unsigned spin_limit = kSpinLimit;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // sharded search: the side stream of the record exchange and the event
+    // rings that hand steps over between the two streams
+    hipStream_t stream_b = nullptr;
+    hipEvent_t ev_a[kEvRing] = {}, ev_b[kEvRing] = {};
+    DevBuf<XState> xstate;
+    DevBuf<StepStats> stats_b;         // the insert kernel's step statistics
+    DevBuf<unsigned char> xsend, xrecv;  // [2][G] and [G] blocks of xblock_bytes
+    // the exchange block in use (sized per round from the demand seen, up
+    // to the allocated maximum) and the fixed stride between the send areas
+    unsigned long long xblock_bytes = 0, xblock_recs = 0, xblock_recs_max = 0, xarea = 0;
+    unsigned long long xblock_learned = 0;  // the block size the last completed search ended with
 
     // problem
     int n = 0, npairs = 0, kw = 1;
@@ -311,8 +324,7 @@ struct pastar_ctx {
     DevBuf<Ctl> ctl;
     DevBuf<unsigned long long> stamps;
     DevBuf<int> goal;
-    DevBuf<uint8_t> outbox, inbox;
-    DevBuf<unsigned long long> xcounts;  // [2 * n_shards] send / recv counts
+    DevBuf<uint8_t> outbox;  // rings of records for the other shards
     Ctl *h_ctl = nullptr;                 // pinned
     bool searched = false;
     bool walk_ready = false;  // one shard: the search already walked the goal's chain (h_walk_masks, h_walk info)
@@ -353,7 +365,6 @@ struct pastar_ctx {
     size_t h_walk_masks_n = 0;
     unsigned char *h_stage = nullptr;  // pinned: per-search uploads (Ctl, origin record)
     DevBuf<unsigned long long> census;  // open-list census of a search
-    unsigned char *h_gather = nullptr;  // pinned: a sharded step's gathered values
 };
 
 namespace {
@@ -557,6 +568,8 @@ struct Ops {
     void (*expand)(dim3, dim3, hipStream_t, const SearchArgs &);
     void (*expand_one_shard)(dim3, dim3, hipStream_t, const SearchArgs &);
     void (*insert_remote)(dim3, dim3, hipStream_t, const SearchArgs &, const void *, unsigned long long);
+    void (*xpack)(dim3, dim3, hipStream_t, const XArgs &);
+    void (*xinsert)(dim3, dim3, hipStream_t, const SearchArgs &, const XArgs &);
     void (*walk)(hipStream_t, const DevProblem *, const uint64_t *, uint64_t, const uint64_t *, int, int, int32_t *,
                  uint64_t *, int *, const int *);
     void (*lookup)(hipStream_t, const uint64_t *, uint64_t, const uint64_t *, uint64_t *);
@@ -583,6 +596,14 @@ struct Impl {
     {
         hipLaunchKernelGGL((insert_remote_kernel<KW>), g, b, 0, s, a, (const Remote<KW> *)recs, count);
     }
+    static void xpack(dim3 g, dim3 b, hipStream_t s, const XArgs &t)
+    {
+        hipLaunchKernelGGL((xpack_kernel<KW>), g, b, 0, s, t);
+    }
+    static void xinsert(dim3 g, dim3 b, hipStream_t s, const SearchArgs &a, const XArgs &t)
+    {
+        hipLaunchKernelGGL((xinsert_kernel<KW>), g, b, 0, s, a, t);
+    }
     static void walk(hipStream_t s, const DevProblem *P, const uint64_t *t, uint64_t cm, const uint64_t *start, int max,
                      int local, int32_t *masks, uint64_t *last, int *info, const int *gate)
     {
@@ -604,7 +625,7 @@ struct Impl {
     {
         hipLaunchKernelGGL((lookup_kernel<KW>), dim3(1), dim3(1), 0, s, t, cm, key, out);
     }
-    static Ops ops() { return Ops{expand_api, expand, expand_one_shard, insert_remote, walk, lookup, tail}; }
+    static Ops ops() { return Ops{expand_api, expand, expand_one_shard, insert_remote, xpack, xinsert, walk, lookup, tail}; }
 };
 
 template <int KW>
@@ -695,6 +716,20 @@ int pastar_rccl_unique_id(unsigned char out[128])
     return PASTAR_OK;
 }
 
+// The side stream of the sharded search and its hand-over events (default
+// priority, like the main stream).
+static int create_side_stream(pastar_ctx *c)
+{
+    if (c->stream_b)
+        return PASTAR_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream_b, hipStreamNonBlocking));
+    for (int k = 0; k < kEvRing; k++) {
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_a[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_b[k], hipEventDisableTiming));
+    }
+    return PASTAR_OK;
+}
+
 int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int shard_rank, const void *rccl_id,
                       pastar_ctx **out)
 {
@@ -738,14 +773,20 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
             return fail(PASTAR_EINVAL, "rccl_id required for n_shards > 1");
         ncclUniqueId id;
         std::memcpy(&id, rccl_id, sizeof(id));
-        ncclComm_t comm = nullptr;
+        ncclComm_t comm = nullptr, xcomm = nullptr;
         NCCL_TRY(ncclCommInitRank(&comm, n_shards, id, shard_rank));
-        c->tr.reset(new RcclTransport(comm));
-        PA_TRY(c->xred.alloc((size_t)(n_shards + 1) * kGatherMax));
+        // the record exchange's own communicator (same ranks); without it the
+        // exchange shares comm, which is still correct: the search's two
+        // streams never both hold RCCL work at once
+        if (ncclCommSplit(comm, 0, shard_rank, &xcomm, nullptr) != ncclSuccess)
+            xcomm = nullptr;
+        c->tr.reset(new RcclTransport(comm, xcomm));
+        PA_TRY(c->xred.alloc(64));
     }
+    if (c->tr)
+        PA_TRY(create_side_stream(c.get()));
     HIP_TRY(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl) + 64, hipHostMallocDefault));  // + pinned scratch
     HIP_TRY(hipHostMalloc((void **)&c->h_stage, sizeof(Ctl) + 256, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void **)&c->h_gather, sizeof(int64_t) * 8 * kGatherMax, hipHostMallocDefault));
     *out = c.release();
     return PASTAR_OK;
 }
@@ -757,7 +798,17 @@ void pastar_gpu_destroy(pastar_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
+    if (c->stream_b)
+        (void)hipStreamSynchronize(c->stream_b);
     c->tr.reset();
+    for (int k = 0; k < kEvRing; k++) {
+        if (c->ev_a[k])
+            (void)hipEventDestroy(c->ev_a[k]);
+        if (c->ev_b[k])
+            (void)hipEventDestroy(c->ev_b[k]);
+    }
+    if (c->stream_b)
+        (void)hipStreamDestroy(c->stream_b);
     for (int gi = 0; gi < 4; gi++) {
         if (c->step_exec[gi])
             (void)hipGraphExecDestroy(c->step_exec[gi]);
@@ -770,8 +821,6 @@ void pastar_gpu_destroy(pastar_ctx *c)
         (void)hipHostFree(c->h_stage);
     if (c->h_walk)
         (void)hipHostFree(c->h_walk);
-    if (c->h_gather)
-        (void)hipHostFree(c->h_gather);
     if (c->h_walk_masks)
         (void)hipHostFree(c->h_walk_masks);
     if (c->h_solo)
@@ -1022,6 +1071,8 @@ namespace {
 
 struct SearchCfg {
     unsigned long long kmax, kmin, pool_entries, subqueue_entries, outbox_cap;
+    unsigned long long xblock_recs;  // records per destination one step's exchange carries
+    int xlag;                        // steps the select may run ahead of the insert of received records (0, 1)
     int table_log2;
     int verbose, profile, eager, depth;
     int64_t max_steps;
@@ -1074,15 +1125,25 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
         c->queues_clean_known = false;
     }
     if (c->tr) {
-        const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * remote_bytes(c->kw);
+        const size_t rb = remote_bytes(c->kw);
+        const size_t bytes = (size_t)c->n_shards * cfg.outbox_cap * rb;
         if (c->outbox.n < bytes) {
             c->outbox.reset();
-            c->inbox.reset();
             PA_TRY(c->outbox.alloc(bytes));
-            PA_TRY(c->inbox.alloc(bytes));
         }
-        if (!c->xcounts.p)
-            PA_TRY(c->xcounts.alloc((size_t)2 * c->n_shards));
+        c->xblock_recs_max = cfg.xblock_recs;
+        const size_t area = (size_t)c->n_shards * ((sizeof(XHdr) + cfg.xblock_recs * rb + 255) & ~(size_t)255);
+        c->xarea = area;
+        if (c->xsend.n < 2 * area) {
+            c->xsend.reset();
+            c->xrecv.reset();
+            PA_TRY(c->xsend.alloc(2 * area));
+            PA_TRY(c->xrecv.alloc(area));
+        }
+        if (!c->xstate.p) {
+            PA_TRY(c->xstate.alloc(1));
+            PA_TRY(c->stats_b.alloc(1));
+        }
     }
     c->cap_log2 = cfg.table_log2;
     c->cap_kmax = cfg.kmax;
@@ -1287,6 +1348,12 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
+    hc.low_b = kBuckets;
+    // (kinase at 8 shards: 147 steps at 4 buckets, 124 at 8; syn8x400: 10.9 M
+    // expansions at 4, 19 M at 8; tools/gpu/probe_shards.py)
+    hc.xwindow = c->n <= 6 ? 2 * kWide : kWide;
+    if (const char *e = std::getenv("PASTAR_XCHG_WINDOW"))  // tuning override
+        hc.xwindow = std::max(1, std::atoi(e));
     const bool seed_batch = c->tr == nullptr;
     if (seed_batch) {
         // one shard: the first batch is the origin alone, staged as select
@@ -1336,6 +1403,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     a.goal_g = c->goal.p;
     a.outbox = c->outbox.p;
     a.outbox_cap = cfg.outbox_cap;
+    a.lower = &c->ctl.p->cur_b;
+    a.x = c->tr ? c->xstate.p : nullptr;
+    a.step = 0;
     a.maxch = maxch_of(cfg);
     a.pool_chunks = c->pool.n / kChunk;
 
@@ -1368,11 +1438,15 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         ops.insert_remote(dim3(1), blk, c->stream, a, drec, 1);
         PA_TRY(check_launch());
     }
-    if (sharded)
+    if (sharded) {
+        HIP_TRY(hipMemsetAsync(c->xstate.p, 0, sizeof(XState), c->stream));
+        HIP_TRY(hipMemsetAsync(c->stats_b.p, 0, sizeof(StepStats), c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        PA_TRY(c->tr->xchg_setup(c));
+    }
 
     double expand_ms = 0;
-    int64_t launches = 0, exchanged = 0;
+    int64_t launches = 0, exchanged = 0, xchg_backlog_steps = 0, xchg_backlog_max = 0, host_waits = 0;
     Ctl h{};
     c->graph_used = false;
     const double t0 = now_s();
@@ -1571,74 +1645,148 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         c->graph_used = use_graph;
         PA_TRY(rc);
     } else {
-        // one host round trip and one small collective per step: every
-        // shard publishes {records for each shard, goal g, had work, failed}
-        // in a single allgather, then the records move by grouped
-        // point-to-point sends and are relaxed on their owner
-        std::vector<unsigned long long> send(G), recv(G), roff(G + 1);
-        std::vector<int64_t> all((size_t)G * (G + 3));
-        int32_t *h_goal = reinterpret_cast<int32_t *>(c->h_ctl + 1);  // pinned scratch after the Ctl copy
-        int64_t *dmine = c->xred.p;  // [G + 3] packed on the device
+        // The sharded step protocol, device-driven: the host only enqueues.
+        //   main stream   [wait: insert of step i - 1 - lag]  select(i), expand(i)
+        //   side stream   [wait: expand(i)]  pack(i), all-to-all(i), insert(i)
+        // Every per-step value (record counts, goals, had-work and failure
+        // flags) travels in the block headers and is consumed on the device,
+        // so the host waits once per round of S steps, for the control block.
+        // lag 0: the next select sees this step's received records; lag 1: it
+        // runs beside their exchange and insert (they reach the select after).
+        const int lag = cfg.xlag;
+        XArgs t{};
+        t.x = c->xstate.p;
+        t.ctl = c->ctl.p;
+        t.stats_b = c->stats_b.p;
+        t.goal_g = c->goal.p;
+        t.fault = c->fault.p;
+        t.outbox = c->outbox.p;
+        t.outbox_cap = cfg.outbox_cap;
+        t.recv = c->xrecv.p;
+        t.n_shards = G;
+        t.shard = c->shard;
+        t.lag = lag;
+        SearchArgs ab = a;  // the insert kernel's arguments: its own statistics, the low_b word
+        ab.stats = c->stats_b.p;
+        ab.lower = &c->ctl.p->low_b;
+        // the block of a round: a power of two of records, sized from the
+        // most any shard had to send in a step of the round before (every
+        // shard folds the same headers, so every shard picks the same size)
+        auto set_block = [&](unsigned long long recs) {
+            recs = std::max<unsigned long long>(1, std::min(recs, c->xblock_recs_max));
+            c->xblock_recs = recs;
+            c->xblock_bytes = (sizeof(XHdr) + recs * rb + 255) & ~(unsigned long long)255;
+            t.block_recs = recs;
+            t.block_bytes = c->xblock_bytes;
+        };
+        // (the first round starts from the size the last search on this
+        // context ended with)
+        set_block(c->xblock_learned ? c->xblock_learned : std::min<unsigned long long>(8192, c->xblock_recs_max));
+        if (std::getenv("PASTAR_XCHG_FIXED"))
+            set_block(c->xblock_recs_max);
+        long long step = 0;
+        int rounds = 0;
+        bool resized = true;
         for (;;) {
-            hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
-            ops.expand(expand_grid, blk, c->stream, a);
-            hipLaunchKernelGGL(step_pack_kernel, dim3(1), dim3(64), 0, c->stream, a,
-                               (unsigned long long)cfg.outbox_cap, dmine);
-            PA_TRY(check_launch());
-            // the step's only host round trip
-            PA_TRY(c->tr->gather_step(c, dmine, G + 3, all.data()));
-            launches++;
-            const int64_t *own = &all[(size_t)c->shard * (G + 3)];
-            const int goal_local = (int)own[G];
-            const bool own_fail = own[G + 2] != 0;
-            int goal_g = goal_local;
-            int64_t any_work = 0, any_fail = 0;
-            for (int sh = 0; sh < G; sh++) {
-                const int64_t *r = &all[(size_t)sh * (G + 3)];
-                recv[sh] = (unsigned long long)r[c->shard];
-                goal_g = std::min<int64_t>(goal_g, r[G]);
-                any_work |= r[G + 1];
-                any_fail |= r[G + 2];
-            }
-            // a capacity failure on any shard stops every shard
-            if (any_fail) {
-                if (!own_fail) {
-                    c->last_fail_mask = 0;
-                    return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
-                }
-                break;
-            }
-            // termination: no shard found a live bucket below the best goal
-            // in this step (then nothing was expanded or sent anywhere)
-            if (!any_work)
-                break;
-            if (goal_g < goal_local) {
-                // before insert_remote, whose own finds can only lower it
-                *h_goal = goal_g;
-                HIP_TRY(hipMemcpyAsync(c->goal.p, h_goal, 4, hipMemcpyHostToDevice, c->stream));
-            }
-            for (int d = 0; d < G; d++)
-                send[d] = (unsigned long long)own[d];
-            roff[0] = 0;
-            for (int d = 0; d < G; d++)
-                roff[d + 1] = roff[d] + recv[d];
-            PA_TRY(c->tr->exchange_records(c, send.data(), recv.data(), roff.data(), rb, cfg.outbox_cap));
-            for (int d = 0; d < G; d++)
-                exchanged += (int64_t)send[d];
-            const unsigned long long total = roff[G];
-            if (total) {
-                const unsigned long long blocks = std::min<unsigned long long>(4096, (total + kBlock - 1) / kBlock);
-                ops.insert_remote(dim3((unsigned)blocks), blk, c->stream, a, c->inbox.p, total);
+            const unsigned pack_y =
+                (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(32, (c->xblock_recs + 4095) / 4096));
+            const unsigned ins_blocks = (unsigned)std::max<unsigned long long>(
+                1, std::min<unsigned long long>(1024, ((unsigned long long)G * c->xblock_recs + kBlock - 1) / kBlock));
+            // steps this round: what the last search on this context predicts
+            // is left (every shard counts the same steps), 16 without one
+            // (short rounds while the block size is still following the demand)
+            int S = resized ? 8 : 16;
+            if (c->last_steps > 0)
+                S = (int)std::min<long long>(64, std::max<long long>(4, c->last_steps + 1 - step));
+            if (const char *e = std::getenv("PASTAR_XCHG_ROUND"))
+                S = std::max(1, std::atoi(e));
+            for (int k = 0; k < S; k++, step++) {
+                const int ring = (int)(step % kEvRing);
+                if (step - 1 - lag >= 0)
+                    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_b[(step - 1 - lag) % kEvRing], 0));
+                a.step = (int)(step & 0x3fffffff);
+                hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
+                ops.expand(expand_grid, blk, c->stream, a);
                 PA_TRY(check_launch());
+                HIP_TRY(hipEventRecord(c->ev_a[ring], c->stream));
+                HIP_TRY(hipStreamWaitEvent(c->stream_b, c->ev_a[ring], 0));
+                t.step = a.step;
+                t.send = c->xsend.p + (size_t)(step & 1) * c->xarea;
+                ops.xpack(dim3((unsigned)G, pack_y), blk, c->stream_b, t);
+                PA_TRY(check_launch());
+                PA_TRY(c->tr->xchg(c, (int)(step & 0x3fffffff)));
+                ops.xinsert(dim3(ins_blocks), blk, c->stream_b, ab, t);
+                PA_TRY(check_launch());
+                HIP_TRY(hipEventRecord(c->ev_b[ring], c->stream_b));
             }
-            if (cfg.verbose && launches % 50 == 0)
-                std::fprintf(stderr, "[pastar %d/%d] step %lld goal %d exchanged %lld\n", c->shard, G,
-                             (long long)launches, goal_g, (long long)exchanged);
+            // the round's one host wait: the control block as the last insert left it
+            HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream_b));
+            {
+                const double t_wait = now_s();
+                hipError_t q;
+                unsigned spin = 0;
+                while ((q = hipStreamQuery(c->stream_b)) == hipErrorNotReady) {
+                    if ((++spin & 15) == 0 && now_s() - t_wait > host_wait_limit_s()) {
+                        const hipError_t qa = hipStreamQuery(c->stream);
+                        return fail(PASTAR_EDEVWAIT, "shard %d: the side stream did not finish the round ending at step "
+                                    "%lld within %.0f s (main stream: %s); the launches are abandoned", c->shard, step,
+                                    host_wait_limit_s(), hipGetErrorString(qa));
+                    }
+                }
+                if (q != hipSuccess)
+                    return fail(PASTAR_ENODEV, "sharded steps failed: %s", hipGetErrorString(q));
+            }
+            rounds++;
+            h = *c->h_ctl;
+            if (h.status)
+                break;
+            {
+                // next round's block: 1.25 x the largest demand of one
+                // (sender, destination) pair, between 4096 records and the allocation
+                unsigned long long demand = 0;
+                HIP_TRY(hipMemcpy(&demand, &c->xstate.p->demand_max, sizeof(demand), hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemsetAsync(&c->xstate.p->demand_max, 0, sizeof(demand), c->stream_b));
+                const unsigned long long want = demand * 5 / 4;
+                unsigned long long recs = 4096;
+                while (recs < want && recs < c->xblock_recs_max)
+                    recs <<= 1;
+                // (shrinks only by one size a round: a quiet round between two busy ones keeps most of the block)
+                if (recs < c->xblock_recs / 2)
+                    recs = c->xblock_recs / 2;
+                if (std::getenv("PASTAR_XCHG_FIXED"))  // tuning probe: always the largest block
+                    recs = c->xblock_recs_max;
+                resized = recs != c->xblock_recs;
+                set_block(recs);
+            }
+            if (cfg.verbose)
+                std::fprintf(stderr, "[pastar %d/%d] step %lld expanded %llu bucket %d status %d (%.3f s)\n", c->shard, G,
+                             step, h.expanded, h.cur_b, h.status, now_s() - t0);
         }
-        // the control block once, after the last step (status, totals)
-        HIP_TRY(hipMemcpyAsync(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        if (cfg.verbose)
+            std::fprintf(stderr, "[pastar %d/%d] loop ends at step %lld: status %d fail mask 0x%x (%.3f s)\n", c->shard, G,
+                         step, h.status, h.fail_mask, now_s() - t0);
+        // the main stream may still hold steps enqueued past the end (they
+        // leave at once); then the totals as both streams left them
         HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(c->h_ctl, c->ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost));
         h = *c->h_ctl;
+        XState xs;
+        HIP_TRY(hipMemcpy(&xs, c->xstate.p, sizeof(XState), hipMemcpyDeviceToHost));
+        exchanged = (int64_t)xs.sent;
+        xchg_backlog_steps = (int64_t)xs.backlog_steps;
+        xchg_backlog_max = (int64_t)xs.backlog_max;
+        host_waits = rounds;
+        h.claimed += xs.claimed_b;
+        if (h.status == 1) {
+            c->last_steps = h.steps;
+            c->xblock_learned = c->xblock_recs;
+        }
+        if (h.status == 2 && !(h.fail_mask & 0xfff)) {
+            // only another shard ran out of capacity
+            c->last_fail_mask = 0;
+            return fail(PASTAR_ENOMEM, "another shard exhausted its device capacity");
+        }
+        h.fail_mask &= 0xfff;
     }
     const double t1 = now_s();
     if (h.status == 2) {
@@ -1712,6 +1860,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     res->table_used = (int64_t)h.claimed;
     res->steps = h.steps;
     res->exchanged = exchanged;
+    res->xchg_backlog_steps = xchg_backlog_steps;
+    res->xchg_backlog_max = xchg_backlog_max;
+    res->host_waits = host_waits;
     res->seconds = t1 - t0;
     {
         const unsigned long long ticks = h.expand_ticks, timed = h.timed_launches;
@@ -1968,6 +2119,13 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     // (round 2: 262144 up to N = 6, kinase 16.7 -> 15.2 ms, narrower inputs
     // flat; profiles/r2_tune_batch.txt)
     cfg.kmax = o.batch_nodes > 0 ? (unsigned long long)o.batch_nodes : (c->n <= 6 ? 262144ull : 65536ull);
+    // sharded: the shards together take about twice the one-shard batch per
+    // step.  A fat bucket is expanded in slices, and what one slice relaxes
+    // spares the next slices the nodes it improves; G full-size slices at
+    // once expand those nodes too (syn8x400 at 8 shards: 10.5 M expansions at
+    // 65536 a shard, 6.6 M at 16384, 5.8 M on one shard)
+    if (o.batch_nodes <= 0 && c->n_shards > 1)
+        cfg.kmax = std::max<unsigned long long>(4096, 2 * cfg.kmax / (unsigned long long)c->n_shards);
     cfg.kmin = o.batch_min > 0 ? std::min<unsigned long long>((unsigned long long)o.batch_min, cfg.kmax) : cfg.kmax / 8;
     // default node-table size: learned from the last search on this context
     // (a repeated search of the same problem initialises only what it
@@ -1982,11 +2140,30 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     // (the pool is never cleared: its size costs memory only, 2 GB here)
     cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 28);
     cfg.subqueue_entries = o.subqueue_entries > 0 ? (unsigned long long)o.subqueue_entries : (1ull << 20);
-    cfg.outbox_cap = std::max<unsigned long long>(1ull << 16, cfg.kmax * masks / std::max(1, c->n_shards));
+    // the ring of records for one destination shard: a power of two, at
+    // least four exchange blocks (what a step cannot send waits in the ring)
+    cfg.xblock_recs = o.xchg_block_records > 0 ? (unsigned long long)o.xchg_block_records : (1ull << 20);
+    if (const char *e = std::getenv("PASTAR_XCHG_BLOCK"))  // tuning override
+        cfg.xblock_recs = std::max(1ull, std::strtoull(e, nullptr, 10));
+    if (cfg.xblock_recs > (1ull << 24))
+        return fail(PASTAR_EINVAL, "xchg_block_records %llu above 2^24", cfg.xblock_recs);
+    cfg.xlag = o.xchg_lag;
+    if (const char *e = std::getenv("PASTAR_XCHG_LAG"))  // tuning override
+        cfg.xlag = std::atoi(e);
+    if (cfg.xlag < 0 || cfg.xlag > 1)
+        return fail(PASTAR_EINVAL, "xchg_lag %d outside [0, 1]", cfg.xlag);
+    cfg.outbox_cap = std::max<unsigned long long>({1ull << 16, cfg.kmax * masks / std::max(1, c->n_shards),
+                                                   2 * cfg.xblock_recs});
     cfg.table_log2 = std::max(cfg.table_log2, c->grown_log2);
     cfg.pool_entries = std::max(cfg.pool_entries, c->grown_pool);
     cfg.subqueue_entries = std::max(cfg.subqueue_entries, c->grown_maxch * (unsigned long long)kChunk);
     cfg.outbox_cap = std::max(cfg.outbox_cap, c->grown_outbox);
+    {
+        unsigned long long p2 = 1;
+        while (p2 < cfg.outbox_cap)
+            p2 <<= 1;
+        cfg.outbox_cap = p2;
+    }
     cfg.verbose = o.verbose;
     cfg.profile = o.profile;
     cfg.eager = o.eager;
@@ -2079,6 +2256,8 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
         res->subqueue_entries = (int64_t)cfg.subqueue_entries;
         res->graph_replay = c->graph_used ? 1 : 0;
     }
+    if (rc != PASTAR_OK && rc != PASTAR_ENOMEM && c->tr)
+        c->tr->abort();  // (a capacity failure is agreed on by every shard: nobody is left waiting)
     return rc;
 }
 
@@ -2205,7 +2384,7 @@ namespace {
 
 int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
 {
-    int64_t *d = c->xred.p;  // kGatherMax * 8 values, persistent
+    int64_t *d = c->xred.p;  // 64 values, persistent
     HIP_TRY(hipMemcpyAsync(d, vals, sizeof(int64_t) * count, hipMemcpyHostToDevice, c->stream));
     const ncclRedOp_t nop = op == kRedSum ? ncclSum : (op == kRedMin ? ncclMin : ncclMax);
     NCCL_TRY(ncclAllReduce(d, d, (size_t)count, ncclInt64, nop, comm_, c->stream));
@@ -2214,29 +2393,20 @@ int RcclTransport::allreduce(pastar_ctx *c, int64_t *vals, int count, RedOp op)
     return PASTAR_OK;
 }
 
-int RcclTransport::gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all)
+int RcclTransport::xchg(pastar_ctx *c, int step)
 {
     const int G = c->n_shards;
-    int64_t *d = c->xred.p + kGatherMax;  // [G][kGatherMax] after the own-values row
-    int64_t *h = reinterpret_cast<int64_t *>(c->h_gather);
-    NCCL_TRY(ncclAllGather(dev_mine, d, (size_t)count, ncclInt64, comm_, c->stream));
-    HIP_TRY(hipMemcpyAsync(h, d, sizeof(int64_t) * count * G, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    std::memcpy(all, h, sizeof(int64_t) * count * G);
-    return PASTAR_OK;
-}
-
-int RcclTransport::exchange_records(pastar_ctx *c, const unsigned long long *send, const unsigned long long *recv,
-                                    const unsigned long long *roff, size_t rb, size_t outbox_cap)
-{
+    const size_t bb = c->xblock_bytes;
+    unsigned char *send = c->xsend.p + (size_t)(step & 1) * c->xarea;
+    ncclComm_t comm = xcomm_ ? xcomm_ : comm_;
     NCCL_TRY(ncclGroupStart());
-    for (int d = 0; d < c->n_shards; d++) {
-        if (d == c->shard)
+    for (int d = 0; d < G; d++) {
+        // (a one-rank communicator exchanges its own, empty, block with
+        // itself, so that this path runs whatever the world size)
+        if (d == c->shard && G > 1)
             continue;
-        if (send[d])
-            NCCL_TRY(ncclSend(c->outbox.p + (size_t)d * outbox_cap * rb, send[d] * rb, ncclUint8, d, comm_, c->stream));
-        if (recv[d])
-            NCCL_TRY(ncclRecv(c->inbox.p + roff[d] * rb, recv[d] * rb, ncclUint8, d, comm_, c->stream));
+        NCCL_TRY(ncclSend(send + (size_t)d * bb, bb, ncclUint8, d, comm, c->stream_b));
+        NCCL_TRY(ncclRecv(c->xrecv.p + (size_t)d * bb, bb, ncclUint8, d, comm, c->stream_b));
     }
     NCCL_TRY(ncclGroupEnd());
     return PASTAR_OK;
@@ -2248,28 +2418,33 @@ int RcclTransport::broadcast(pastar_ctx *c, void *dev, size_t bytes, int root)
     return PASTAR_OK;
 }
 
-int LocalTransport::gather_step(pastar_ctx *c, const int64_t *dev_mine, int count, int64_t *all)
+int LocalTransport::xchg_setup(pastar_ctx *c)
 {
-    int64_t *h = reinterpret_cast<int64_t *>(c->h_gather);
-    HIP_TRY(hipMemcpyAsync(h, dev_mine, sizeof(int64_t) * count, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return allgather(h, count, all);
+    if (!g_->ev_pack[rank_][0])
+        for (int k = 0; k < kEvRing; k++)
+            HIP_TRY(hipEventCreateWithFlags(&g_->ev_pack[rank_][k], hipEventDisableTiming));
+    g_->xsend[rank_] = {c->xsend.p, c->xsend.p + c->xarea};
+    g_->device[rank_] = c->device;
+    return sync();  // every shard's addresses and events are published
 }
 
-int LocalTransport::exchange_records(pastar_ctx *c, const unsigned long long *, const unsigned long long *recv,
-                                     const unsigned long long *roff, size_t rb, size_t outbox_cap)
+int LocalTransport::xchg(pastar_ctx *c, int step)
 {
-    g_->outbox[rank_] = c->outbox.p;
-    g_->device[rank_] = c->device;
+    const int G = g_->G, ring = step % kEvRing, par = step & 1;
+    // this shard's blocks are packed once the side stream reaches this event;
+    // the host barrier orders every shard's record before any shard's wait
+    HIP_TRY(hipEventRecord(g_->ev_pack[rank_][ring], c->stream_b));
     PA_TRY(sync());
-    for (int s = 0; s < g_->G; s++) {
-        if (s == rank_ || !recv[s])
-            continue;
-        const uint8_t *src = g_->outbox[s] + (size_t)rank_ * outbox_cap * rb;
-        HIP_TRY(hipMemcpyPeerAsync(c->inbox.p + roff[s] * rb, c->device, src, g_->device[s], recv[s] * rb, c->stream));
+    XPeers p{};
+    for (int s = 0; s < G; s++) {
+        p.src[s] = g_->xsend[s][par] + (size_t)rank_ * c->xblock_bytes;
+        if (s != rank_)
+            HIP_TRY(hipStreamWaitEvent(c->stream_b, g_->ev_pack[s][ring], 0));
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return sync();  // peers may refill their outboxes only after every copy
+    const unsigned y = (unsigned)std::max<unsigned long long>(1, std::min<unsigned long long>(32, (c->xblock_recs + 4095) / 4096));
+    hipLaunchKernelGGL(xcopy_kernel, dim3((unsigned)G, y), dim3(kBlock), 0, c->stream_b, p, c->xrecv.p,
+                       c->xblock_bytes, (unsigned long long)remote_bytes(c->kw), rank_);
+    return check_launch();
 }
 
 int LocalTransport::broadcast(pastar_ctx *c, void *dev, size_t bytes, int root)
@@ -2297,7 +2472,10 @@ int pastar_group_create(int n_shards, pastar_group **out)
     g->G = n_shards;
     g->vals.resize(n_shards);
     g->counts.resize(n_shards);
-    g->outbox.resize(n_shards, nullptr);
+    g->xsend.resize(n_shards);
+    g->ev_pack.resize(n_shards);
+    for (auto &r : g->ev_pack)
+        r.fill(nullptr);
     g->bufs.resize(n_shards, nullptr);
     g->device.resize(n_shards, 0);
     *out = g;
@@ -2306,6 +2484,12 @@ int pastar_group_create(int n_shards, pastar_group **out)
 
 void pastar_group_destroy(pastar_group *g)
 {
+    if (!g)
+        return;
+    for (auto &r : g->ev_pack)
+        for (hipEvent_t e : r)
+            if (e)
+                (void)hipEventDestroy(e);
     delete g;
 }
 
@@ -2325,9 +2509,10 @@ int pastar_gpu_create_grouped(const pastar_problem *p, int device, pastar_group 
     c->hp.shard = shard_rank;
     HIP_TRY(hipMemcpy(c->dP.p, &c->hp, sizeof(c->hp), hipMemcpyHostToDevice));
     if (group->G > 1) {
-        PA_TRY(c->xred.alloc((size_t)(group->G + 1) * kGatherMax));
+        PA_TRY(c->xred.alloc(64));
         c->tr.reset(new LocalTransport(group, shard_rank));
         group->members++;
+        PA_TRY(create_side_stream(c));
         for (int d = 0; d < 8; d++) {  // peer access for the copies, where the link allows it
             int ok = 0;
             if (d != device && hipDeviceCanAccessPeer(&ok, device, d) == hipSuccess && ok)
@@ -2434,6 +2619,8 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     cfg.pool_entries = o.pool_entries > 0 ? (unsigned long long)o.pool_entries : (1ull << 22);
     cfg.subqueue_entries = o.subqueue_entries > 0 ? (unsigned long long)o.subqueue_entries : (1ull << 18);
     cfg.outbox_cap = 1;
+    cfg.xblock_recs = 1;
+    cfg.xlag = 0;
     PA_TRY(alloc_search(c, cfg));
     int w = c->auto_band_log2;
     if (o.band > 0)
@@ -2447,6 +2634,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     hc.maxch = maxch_of(cfg);
     hc.table_slots = c->nslots;
     hc.cur_b = kBuckets;  // empty: appends lower it
+    hc.low_b = kBuckets;
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
     PA_TRY(init_search(c, cfg, sizeof(Ctl)));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2464,6 +2652,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     a.pool = c->pool.p;
     a.stats = c->stats.p;
     a.goal_g = c->goal.p;
+    a.lower = &c->ctl.p->cur_b;
     a.maxch = maxch_of(cfg);
     a.pool_chunks = c->pool.n / kChunk;
     c->lists_reopen = 0;

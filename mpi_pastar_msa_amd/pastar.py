@@ -129,13 +129,16 @@ class PAStarOpt:
     eager: bool = False
     depth: int = 0
     mode: str = "auto"  # "auto": LDS-resident search when the problem fits; "batched"; "solo"
+    xchg_lag: int = 0   # sharded: 1 = the exchange of step i runs beside the expansion of step i + 1
+    xchg_block_records: int = 0  # sharded: records one step carries to one shard (0 = default)
 
     def search_opts(self):
         return nat.pastar_search_opts(self.batch_nodes, self.batch_min, self.table_slots_log2, self.pool_entries,
                                       self.subqueue_entries, self.max_steps, self.band, int(self.profile),
                                       int(self.verbose),
                                       int(not self.autogrow), int(self.eager), int(self.depth),
-                                      {"auto": 0, "batched": 1, "solo": 2}[self.mode])
+                                      {"auto": 0, "batched": 1, "solo": 2}[self.mode],
+                                      int(self.xchg_lag), 0, int(self.xchg_block_records))
 
 
 def compute_weights(seqs):
@@ -178,6 +181,9 @@ class SearchResult:
     select_ms: float = 0.0
     gap_ms: float = 0.0
     solo: int = 0
+    xchg_backlog_steps: int = 0
+    xchg_backlog_max: int = 0
+    host_waits: int = 0
     extra: dict = field(default_factory=dict)
 
 
