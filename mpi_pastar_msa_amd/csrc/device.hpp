@@ -183,6 +183,7 @@ struct XState {
     unsigned long long demand_max;  // most records one shard had for one destination in a step, since the host's last reset
     unsigned long long claimed_b, dropped_b;  // insert's table claims, folded by pack
     int fail_b, fault_b;
+    unsigned long long steps_done;  // steps up to and including the one that ended the search
     int quiet_run;  // consecutive steps in which no shard had work, records or backlog
     int pad0;
 };
@@ -282,7 +283,9 @@ __device__ __forceinline__ void wave_append(bool pred, unsigned long long *count
 // matched word 0 re-reads a zero tail word until it is written (the claimant
 // writes it in the same loop iteration, so no wave can stall on itself).
 // best only decreases, so a lagging read of it can only skip a relaxation
-// that would not improve anything.
+// that would not improve anything.  *lowered (optional; the caller sets it
+// false) reports that best itself decreased: a better g, or the same g with
+// a smaller parent mask.
 //
 // pre (has_pre): the key words and best of the first PFS slots of the probe
 // sequence, read by the caller ahead of time (slot_prefetch); a read taken
@@ -299,7 +302,7 @@ template <int KW, int PFS>
 __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t cap_mask,
                                          const uint64_t (&key)[KW], int g, int pmask, int h,
                                          bool &improved, bool &claimed, bool has_pre,
-                                         const SlotWords<KW, PFS> &pre)
+                                         const SlotWords<KW, PFS> &pre, bool *lowered = nullptr)
 {
     constexpr int SW = slot_words<KW>();
     improved = false;
@@ -416,9 +419,15 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
             __hip_atomic_fetch_min((unsigned long long *)(s + KW), (unsigned long long)packed, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             improved = true;
+            if (lowered)
+                *lowered = true;
         } else if (packed < wv[KW]) {
             const uint64_t old = atomicMin((unsigned long long *)(s + KW), (unsigned long long)packed);
             improved = (int64_t)(old >> 32) > (int64_t)g || old == ~0ull;
+            // lowered: also a tie on g with a smaller parent mask (no
+            // re-expansion, but the record's mask changed)
+            if (lowered)
+                *lowered = packed < old;
         }
         return (int64_t)idx;
     }

@@ -781,14 +781,19 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
     // the exchange by the number of parents a shard holds of one node.  The
     // owner's table alone is authoritative for the node (open list,
     // closed mark, backtrace).
+    // Ties count: a record with the best g this shard has seen and a
+    // smaller parent mask is sent too, so the owner ends with the smallest
+    // mask over all shards' parents, as the one-shard table does.
     const bool filter = SH && P.n_shards > 1;
+    bool lowered = false;
     if (valid && (local || filter)) {
-        slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre);
+        slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre, &lowered);
         if (slot < 0) {
             if (slot == -2)
                 atomicOr(a.fault, (int)kSiteRelaxTail);
             ovf++;
             improved = false;
+            lowered = false;
         }
         claimed += cl;
         if (improved) {
@@ -850,7 +855,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
     }
     queue_append(a, global, bucket_of(f, f0, w), e, st, remote_in);
     if (SH && P.n_shards > 1) {
-        const bool remote = valid && !local && improved;
+        const bool remote = valid && !local && lowered;
         Remote<KW> rec;
 #pragma unroll
         for (int k = 0; k < KW; k++)
@@ -2190,8 +2195,12 @@ __global__ __launch_bounds__(kBlock) void xinsert_kernel(SearchArgs a, XArgs t)
                 const bool quiet = !work && backlog == 0;
                 const int run = quiet ? x->quiet_run + 1 : 0;
                 x->quiet_run = run;
-                if (run > t.lag)
+                if (run > t.lag) {
+                    // (the step count every shard agrees on: the main
+                    // stream's own counter may be a select ahead)
+                    x->steps_done = (unsigned long long)t.step + 1;
                     ctl->status = 1;
+                }
             }
         }
     }

@@ -1778,6 +1778,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         host_waits = rounds;
         h.claimed += xs.claimed_b;
         if (h.status == 1) {
+            h.steps = (long long)xs.steps_done;  // the same on every shard
             c->last_steps = h.steps;
             c->xblock_learned = c->xblock_recs;
         }

@@ -4,8 +4,10 @@
 The device search shards one A* by the reference's owner hash
 (CoordHash.cpp / Sequences::get_id, z-order by default): every node lives on
 exactly one shard, children are routed to their owner, and each step ends in
-an exchange (counts, then records), a MIN allreduce of the goal g and a SUM
-allreduce of the has-work flags (pastar_gpu.hip, search_impl, G > 1 branch).
+an exchange of fixed-size blocks whose headers carry what the reference's
+check_stop allreduces (goal g, had work) plus the records sent and still
+waiting (pastar_gpu.hip, search_impl, G > 1 branch; kernels.hpp xpack_kernel /
+xinsert_kernel).
 `ShardModel` below restates that protocol step for step on the CPU, with the
 oracle's Node::getNeigh as the expansion and gloo as the transport, so the
 protocol itself (termination rule, goal bound, reopening, owner routing,
@@ -71,12 +73,17 @@ def _entry(rank, world, port, fn, args, q):
 class ShardModel:
     """One shard of the sharded search (search_impl, G > 1): a node table
     (pos -> best g, parent mask, closed), f-bucketed open lists of width
-    2**band_log2 above f0 = h(origin), an outbox per destination shard."""
+    2**band_log2 above f0 = h(origin), and the exchange of csrc/kernels.hpp
+    (xpack / all-to-all / xinsert): a ring of records per destination shard,
+    of which one step carries at most `block` per destination in a
+    fixed-size block behind a header; every shard folds the same headers."""
 
-    def __init__(self, o, rank, world, band_log2, batch):
+    WINDOW = 4  # buckets above the shards' common lowest live bucket a batch may come from
+
+    def __init__(self, o, rank, world, band_log2, batch, block=1 << 20, lag=0):
         self.o, self.rank, self.world = o, rank, world
-        self.band, self.batch = band_log2, batch
-        self.best = {}      # pos -> (g, parenti)
+        self.band, self.batch, self.block, self.lag = band_log2, batch, block, lag
+        self.best = {}      # pos -> (g, parenti): owned nodes, and the best this shard sent of the others'
         self.closed = {}    # pos -> g it was expanded with
         self.buckets = {}   # bucket -> [(pos, g, f, parenti)]
         self.goal_pos = tuple(o.lengths)
@@ -84,32 +91,46 @@ class ShardModel:
         self.f0 = o.initial_node()[2]
         self.expanded = 0
         self.sent = 0
+        self.ring = [[] for _ in range(world)]  # records waiting for each destination
+        self.gmin = 0        # lowest live bucket over all shards, as of their last select
+        self.quiet_run = 0
+        self.backlog_steps = 0
+        self.pending = []    # lag 1: records received, relaxed after the next select
 
     def bucket(self, f):
         return max(0, (f - self.f0) >> self.band)
 
-    def relax(self, node):
-        """relax() in device.hpp: improved iff strictly lower g."""
+    def owner(self, pos):
+        return orc.get_id(list(pos), self.world, 0, 12)
+
+    def relax(self, node, owned=True):
+        """relax() in device.hpp: improved iff strictly lower g.  A node of
+        another shard is relaxed too (route_child's sender-side filter): it
+        is sent only when this shard improved on what it sent before."""
         pos, g, f, par = node
         b = self.best.get(pos)
         if b is not None and b[0] <= g:
-            return
+            return False
         self.best[pos] = (g, par)
         if pos == self.goal_pos:
             self.goal_g = min(self.goal_g, g)
-            return
-        self.buckets.setdefault(self.bucket(f), []).append(node)
+            return not owned
+        if owned:
+            self.buckets.setdefault(self.bucket(f), []).append(node)
+        return True
 
     def step(self):
         """select_kernel + expand_kernel: the lowest live bucket not above the
-        goal's, at most `batch` entries; stale entries (g no longer the
-        best) are dropped.  Returns (had_work, outboxes)."""
-        outbox = [[] for _ in range(self.world)]
+        goal's, if it lies inside the shards' common window; at most `batch`
+        entries; stale entries (g no longer the best) are dropped.  Returns
+        (has_work, lowest live bucket or None)."""
         limit = self.bucket(self.goal_g) if self.goal_g < INT_MAX else None
         live = sorted(b for b, v in self.buckets.items() if v and (limit is None or b <= limit))
         if not live:
-            return 0, outbox
+            return 0, None
         b = live[0]
+        if self.gmin is not None and b > self.gmin + self.WINDOW - 1:
+            return 1, b  # live entries above the window: an idle step
         batch, self.buckets[b] = self.buckets[b][:self.batch], self.buckets[b][self.batch:]
         for node in batch:
             pos, g = node[0], node[1]
@@ -120,53 +141,80 @@ class ShardModel:
             self.closed[pos] = g
             self.expanded += 1
             for kid, owner in self.o.get_neigh(node, self.world, 0, 12):
-                outbox[owner].append(kid)
-        return 1, outbox
+                if owner == self.rank:
+                    self.relax(kid)
+                elif self.relax(kid, owned=False):
+                    self.ring[owner].append(kid)
+        return 1, b
 
-    def exchange(self, outbox):
-        """exchange_counts + exchange_records (the RCCL grouped send/recv)."""
-        n = self.o.n
+    def exchange(self, has_work, low_b):
+        """xpack + the all-to-all + xinsert's header fold.  Every shard sends
+        every shard one block of `block` record slots behind a header
+        {n, sent_all, backlog_all, has_work, goal, low_b}; the fields other
+        than n are the same in all of a sender's blocks.  Returns (records
+        for this shard, headers of all shards)."""
+        n, W, C = self.o.n, self.world, self.block
         width = n + 3
-        counts = torch.tensor([len(v) for v in outbox], dtype=torch.int64)
-        all_counts = [torch.zeros(self.world, dtype=torch.int64) for _ in range(self.world)]
-        dist.all_gather(all_counts, counts)
-        reqs, inbox = [], []
-        for d in range(self.world):
-            if d == self.rank:
-                continue
-            if outbox[d]:
-                t = torch.tensor([list(k[0]) + [k[1], k[2], k[3]] for k in outbox[d]], dtype=torch.int64)
-                reqs.append(dist.isend(t, d))
-                self.sent += len(outbox[d])
-            m = int(all_counts[d][self.rank])
-            if m:
-                t = torch.zeros((m, width), dtype=torch.int64)
-                reqs.append(dist.irecv(t, d))
-                inbox.append(t)
-        for r in reqs:
-            r.wait()
-        recs = list(outbox[self.rank])
-        for t in inbox:
-            recs += [(tuple(row[:n]), row[n], row[n + 1], row[n + 2]) for row in t.tolist()]
-        return recs
+        take = [self.ring[d][:C] for d in range(W)]
+        self.ring = [self.ring[d][C:] for d in range(W)]
+        sent_all = sum(len(t) for t in take)
+        backlog_all = sum(len(r) for r in self.ring)
+        self.sent += sent_all
+        self.backlog_steps += backlog_all > 0
+        # (the model sizes its block tensor to the step's largest block: the
+        # device's blocks are fixed-size, C records, mostly empty)
+        cap_t = torch.tensor([max(len(t) for t in take)], dtype=torch.int64)
+        dist.all_reduce(cap_t, op=dist.ReduceOp.MAX)
+        cap = max(1, int(cap_t))
+        area = torch.zeros((W, 6 + cap * width), dtype=torch.int64)
+        for d in range(W):
+            area[d, :6] = torch.tensor([len(take[d]), sent_all, backlog_all, has_work, self.goal_g,
+                                        -1 if low_b is None else low_b])
+            if take[d]:
+                area[d, 6:6 + len(take[d]) * width] = torch.tensor(
+                    [list(k[0]) + [k[1], k[2], k[3]] for k in take[d]], dtype=torch.int64).reshape(-1)
+        got = [torch.zeros_like(area) for _ in range(W)]
+        dist.all_gather(got, area)  # (rank s's block for this shard is got[s][self.rank])
+        recs, hdrs = [], []
+        for s_ in range(W):
+            blk = got[s_][self.rank]
+            hdrs.append([int(v) for v in blk[:6]])
+            rows = blk[6:6 + int(blk[0]) * width].reshape(-1, width).tolist()
+            recs += [(tuple(row[:n]), row[n], row[n + 1], row[n + 2]) for row in rows]
+        return recs, hdrs
 
-    def search(self):
+    def search(self, max_steps=100000):
         origin = self.o.initial_node()
-        if orc.get_id(list(origin[0]), self.world, 0, 12) == self.rank:
+        if self.owner(origin[0]) == self.rank:
             self.relax(origin)
         steps = 0
-        while True:
-            had, outbox = self.step()
-            for rec in self.exchange(outbox):
-                self.relax(rec)
-            t = torch.tensor([self.goal_g], dtype=torch.int64)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            self.goal_g = int(t)
-            h = torch.tensor([had], dtype=torch.int64)
-            dist.all_reduce(h)
+        while steps < max_steps:
+            has_work, low_b = self.step()
+            if self.lag:  # the records of the step before reach the open list after this select
+                for rec in self.pending:
+                    self.relax(rec)
+                self.pending = []
+            recs, hdrs = self.exchange(has_work, low_b)
+            if self.lag:
+                self.pending = recs
+            else:
+                for rec in recs:
+                    self.relax(rec)
             steps += 1
-            if int(h) == 0:
+            # xinsert's fold: only fields that are the same in all blocks of a sender
+            self.goal_g = min([self.goal_g] + [h[4] for h in hdrs])
+            lows = [h[5] for h in hdrs if h[5] >= 0]
+            self.gmin = min(lows) if lows else None
+            work = any(h[3] or h[1] for h in hdrs)
+            backlog = sum(h[2] for h in hdrs)
+            # termination: nobody had a batch, sent a record or keeps records
+            # in its rings, for lag + 1 steps in a row (records in flight
+            # under lag 1 were sent in the step before: not quiet)
+            self.quiet_run = self.quiet_run + 1 if (not work and backlog == 0) else 0
+            if self.quiet_run > self.lag:
+                assert not self.pending and not any(self.ring)
                 return steps
+        raise RuntimeError("step limit")
 
     def walk(self):
         """walk_kernel + broadcast: the owner of the current node names its
@@ -193,29 +241,39 @@ def rows_from_path(seqs, path):
     return rows
 
 
-def _sharded_search(rank, world, fasta, band_log2, batch):
+def _sharded_search(rank, world, fasta, band_log2, batch, block=1 << 20, lag=0):
     o = orc.Oracle(fasta=fasta)
-    m = ShardModel(o, rank, world, band_log2, batch)
+    m = ShardModel(o, rank, world, band_log2, batch, block, lag)
     steps = m.search()
     goal_owner = orc.get_id(list(m.goal_pos), world, 0, 12)
     path = m.walk()
     rows = rows_from_path(o.seqs, path)
-    # every node has exactly one owner: nothing this shard holds belongs elsewhere
-    foreign = sum(1 for p in m.best if orc.get_id(list(p), world, 0, 12) != rank)
+    # every node has exactly one owner: nothing this shard expanded or queued belongs elsewhere
+    foreign = sum(1 for p in m.closed if orc.get_id(list(p), world, 0, 12) != rank)
+    foreign += sum(1 for v in m.buckets.values() for nd in v if orc.get_id(list(nd[0]), world, 0, 12) != rank)
     return {"goal_g": m.goal_g, "steps": steps, "expanded": m.expanded, "sent": m.sent,
+            "backlog_steps": m.backlog_steps,
             "rows": rows, "cost": o.alignment_cost(rows), "foreign": foreign,
             "goal_owner_has_goal": (rank != goal_owner) or (m.goal_pos in m.best),
             "nodes": len(m.best)}
 
 
-CASES = [("test2", 2, 4, 64), ("PF08184", 2, 6, 16), ("test", 2, 0, 1 << 20),
-         ("test2", 3, 8, 8), ("syn4x200_s1", 2, 13, 4096)]
+# (name, world, band_log2, batch, block records per destination and step, lag)
+CASES = [("test2", 2, 4, 64, 1 << 20, 0), ("PF08184", 2, 6, 16, 1 << 20, 0), ("test", 2, 0, 1 << 20, 1 << 20, 0),
+         ("test2", 3, 8, 8, 1 << 20, 0), ("syn4x200_s1", 2, 13, 4096, 1 << 20, 0),
+         # blocks too small for a step's records (they wait in the rings), and the
+         # exchange running beside the next step's expansion
+         ("test2", 2, 4, 64, 3, 0), ("test2", 3, 8, 8, 2, 1), ("PF08184", 2, 6, 16, 1 << 20, 1),
+         ("syn4x200_s1", 2, 13, 4096, 256, 1)]
 
 
-@pytest.mark.parametrize("name,world,band_log2,batch", CASES)
-def test_sharded_protocol_reaches_reference_optimum(name, world, band_log2, batch, kat):
+@pytest.mark.parametrize("name,world,band_log2,batch,block,lag", CASES)
+def test_sharded_protocol_reaches_reference_optimum(name, world, band_log2, batch, block, lag, kat):
     ref = kat["inputs"][name]
-    res = run_ranks(world, _sharded_search, golden(ref["file"]), band_log2, batch)
+    res = run_ranks(world, _sharded_search, golden(ref["file"]), band_log2, batch, block, lag)
+    assert len({r["steps"] for r in res}) == 1  # every shard stops at the same step
+    if block < 100:
+        assert sum(r["backlog_steps"] for r in res) > 0  # records really waited in a ring
     for r in res:
         assert r["goal_g"] == ref["score"]
         assert r["cost"] == ref["score"]

@@ -252,6 +252,29 @@ def test_sharded_search_one_gpu(name, shards, kat, oracles):
         assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
 
 
+@pytest.mark.parametrize("name,shards,lag,block", [("syn4x200_s1", 4, 1, 0), ("kinase", 4, 1, 0),
+                                                    ("kinase", 8, 0, 4096), ("syn8x100_s3", 8, 1, 8192)])
+def test_sharded_search_overlap_and_small_blocks(name, shards, lag, block, kat):
+    """The exchange beside the next step's expansion (xchg_lag = 1: records
+    reach the open list one select later, termination waits for two quiet
+    steps) and exchange blocks too small for a step's records (they wait in
+    the sender's ring, which holds back its batches): same optimal score,
+    a valid optimal alignment, one host wait per round of steps."""
+    from mpi_pastar_msa_amd import sharded_search
+    ref = kat["inputs"][name]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    res, rows = sharded_search(seqs, shards, opt=PAStarOpt(xchg_lag=lag, xchg_block_records=block))
+    assert [r.score for r in res] == [ref["score"]] * shards
+    assert len({r.steps for r in res}) == 1  # every shard stops at the same step
+    assert all(1 <= r.host_waits <= r.steps // 4 + 1 for r in res)
+    if block:
+        assert sum(r.xchg_backlog_steps for r in res) > 0
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    assert o.alignment_cost(rows) == ref["score"]
+    if "alignment_md5" in ref:
+        assert hashlib.md5("".join(r + "\n" for r in rows).encode()).hexdigest() == ref["alignment_md5"]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("shards,depth,profile", [(8, 1, True), (4, 0, True), (8, 0, False)])
 def test_sharded_search_repeated_exact(shards, depth, profile, kat):
@@ -436,7 +459,14 @@ def test_rccl_transport_world_one(name, kat):
     with Engine(seqs, n_shards=1, shard_rank=0, rccl_id=rccl_unique_id()).init() as e:
         r = e.pa_star(PAStarOpt())
         assert r.score == ref["score"]
-        assert r.graph_replay == 0  # the sharded protocol: host-driven steps
+        assert r.graph_replay == 0
+        # the sharded protocol: the host enqueues rounds of steps and waits
+        # once per round; the blocks travel by RCCL send/recv on the side
+        # stream (a one-rank communicator exchanges its block with itself)
+        assert 1 <= r.host_waits <= r.steps // 4 + 1
+        assert r.exchanged == 0 and r.xchg_backlog_steps == 0
+        r1 = e.pa_star(PAStarOpt(xchg_lag=1))  # the exchange beside the next step's expansion
+        assert r1.score == ref["score"] and 1 <= r1.host_waits <= r1.steps // 4 + 1
         assert e.allreduce([3, 5], "max") == [3, 5]
         e.barrier()
         rows = e.alignment()
