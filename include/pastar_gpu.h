@@ -263,6 +263,20 @@ int pastar_gpu_expand_noalloc(pastar_ctx *ctx, const pastar_node *in, int n_in, 
 /* Device-resident PAStar search from the origin to the final coordinate. */
 int pastar_gpu_search(pastar_ctx *ctx, const pastar_search_opts *opts, pastar_result *res);
 
+/* Many independent searches in ONE launch (no counterpart in the reference,
+ * which aligns one family per process: PAStar::pa_star over many inputs at
+ * once).  Search k runs whole in one workgroup's LDS (the LDS-resident
+ * engine, PASTAR_MODE_SOLO), so every problem must fit it (small families:
+ * PF08184-sized) and all contexts must sit on one device and have the same
+ * number of sequences; count <= 65535 distinct contexts.  results[k] is what
+ * pastar_gpu_search(ctxs[k]) returns (its `seconds` is the whole launch's);
+ * afterwards each context answers pastar_gpu_alignment /
+ * pastar_gpu_closed_lookup for its own search.  A search that outgrows its
+ * LDS node table gets score -1 in results[k] and the call returns
+ * PASTAR_ENOMEM (the others are valid); opts: band, max_steps, verbose. */
+int pastar_gpu_search_many(pastar_ctx *const *ctxs, int count, const pastar_search_opts *opts,
+                           pastar_result *results);
+
 /* ClosedList lookup after a search: the stored node for a coordinate owned by
  * this shard (PASTAR_ENOTFOUND if absent). */
 int pastar_gpu_closed_lookup(pastar_ctx *ctx, const uint16_t *pos, pastar_node *out);

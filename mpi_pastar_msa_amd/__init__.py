@@ -8,8 +8,8 @@ reference interface; see pastar.py.
 """
 from .pastar import (ClosedList, Engine, Node, PriorityList, PAStarOpt, SearchResult, Sequences, compute_weights, cost, get_id,
                      lz4_dec, lz4_en, pack_nodes, unpack_nodes,
-                     rccl_unique_id, sharded_search, similarity, ShardGroup)
+                     rccl_unique_id, search_many, sharded_search, similarity, ShardGroup)
 
 __all__ = ["ClosedList", "Engine", "Node", "PriorityList", "PAStarOpt", "SearchResult", "Sequences", "compute_weights", "cost", "get_id",
            "lz4_dec", "lz4_en", "pack_nodes", "unpack_nodes",
-           "rccl_unique_id", "sharded_search", "similarity", "ShardGroup"]
+           "rccl_unique_id", "search_many", "sharded_search", "similarity", "ShardGroup"]

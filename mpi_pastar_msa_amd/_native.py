@@ -141,6 +141,8 @@ SIGNATURES = {
                                                  ctypes.POINTER(ctypes.c_int64)]),
     "pastar_gpu_search": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(pastar_search_opts),
                                          ctypes.POINTER(pastar_result)]),
+    "pastar_gpu_search_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                              ctypes.POINTER(pastar_search_opts), ctypes.POINTER(pastar_result)]),
     "pastar_gpu_closed_lookup": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint16),
                                                 ctypes.POINTER(pastar_node)]),
     "pastar_gpu_alignment": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int,

@@ -55,6 +55,7 @@ static __device__ __align__(256) unsigned char scratch[kScratchBytes];
 namespace {
 
 thread_local std::string g_err;
+std::atomic<uint64_t> g_many_stamp{0};
 
 int fail(int code, const char *fmt, ...)
 {
@@ -300,6 +301,16 @@ struct pastar_ctx {
     bool solo_failed = false;  // a solo search of this problem overflowed its LDS capacity
     bool solo_active = false;  // the last search ran on the solo path (its node table is solo_dump)
     unsigned solo_attr_done = 0;  // per N: dynamic LDS limit raised
+    unsigned solo_many_attr_done = 0;
+    // pastar_gpu_search_many: this context's launch record as last prepared
+    // (valid while its options and buffers stay the same)
+    bool many_cached = false;
+    long long many_band = 0, many_max_steps = 0;
+    SoloArgs many_a{};
+    uint64_t many_stamp = 0;
+    size_t many_lds = 0;
+    volatile uint32_t *many_done = nullptr;
+    DevBuf<unsigned char> many_args;  // pastar_gpu_search_many: the launch's argument records
     DevBuf<uint64_t> solo_dump;   // the solo node table in the main slot layout
     int solo_cap_log2 = 0;
     unsigned char *h_solo = nullptr;  // pinned: SoloOut + backtrace masks, written by the kernel
@@ -1972,9 +1983,29 @@ const void *solo_fn_for(int n)
     }
 }
 
-// Returns PASTAR_ENOMEM when the search outgrew the LDS node table (the
-// caller then runs the batched engine).
-int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result *res)
+template <int N>
+const void *solo_many_fn()
+{
+    return (const void *)solo_many_kernel<N>;
+}
+
+const void *solo_many_fn_for(int n)
+{
+    switch (n) {
+    case 2: return solo_many_fn<2>();
+    case 3: return solo_many_fn<3>();
+    case 4: return solo_many_fn<4>();
+    case 5: return solo_many_fn<5>();
+    case 6: return solo_many_fn<6>();
+    case 7: return solo_many_fn<7>();
+    default: return solo_many_fn<8>();
+    }
+}
+
+// The kernel arguments of one LDS-resident search on context c, its result
+// areas (pinned host memory, the node-table dump) made ready; *done_out is
+// the host view of the completion word, cleared.
+int solo_prepare(pastar_ctx *c, const SearchCfg &cfg, const SoloPlan &pl, SoloArgs *out, volatile uint32_t **done_out)
 {
     int total_len = 0;
     for (int i = 0; i < c->n; i++)
@@ -1992,6 +2023,7 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
         c->h_solo_n = 0;
         HIP_TRY(hipHostMalloc((void **)&c->h_solo, out_bytes, hipHostMallocDefault));
         c->h_solo_n = out_bytes;
+        c->many_cached = false;  // (a cached launch record points into the old area)
     }
     PA_TRY(ensure_walk_buffers(c, total_len));
     SoloArgs a = pl.a;
@@ -2017,35 +2049,42 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
         PA_TRY(estimate_band_log2(c, 0, cfg.band, &w));
         a.band_log2 = w;
     }
-    const void *fn = solo_fn_for(c->n);
-    if (!(c->solo_attr_done & (1u << c->n))) {
-        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSoloLds));
-        c->solo_attr_done |= 1u << c->n;
-    }
-    void *args[] = {(void *)&a};
-    const double t0 = now_s();
-    HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(kSoloThreads), args, pl.lds, c->stream));
-    PA_TRY(check_launch());
-    // wait by watching the completion word (the kernel's last store) rather
-    // than for the stream's completion signal, a few microseconds later; the
-    // stream is still polled, so a failed launch ends the wait with its error
-    for (unsigned spin = 1; *done != a.ticket; spin++) {
+    *out = a;
+    *done_out = done;
+    return PASTAR_OK;
+}
+
+// Wait for a completion word (the kernel's last store) rather than for the
+// stream's completion signal, a few microseconds later; the stream is still
+// polled, so a failed launch ends the wait with its error.
+int solo_wait(hipStream_t stream, volatile uint32_t *done, uint32_t ticket, double t0)
+{
+    for (unsigned spin = 1; *done != ticket; spin++) {
         if ((spin & 255) == 0) {
             if ((spin & 0xfffff) == 0 && now_s() - t0 > host_wait_limit_s())
                 return fail(PASTAR_EDEVWAIT, "the LDS-resident search did not report its end within %.0f s "
                             "(PASTAR_WAIT_TIMEOUT_S); the launch is abandoned", host_wait_limit_s());
-            const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess && *done == a.ticket)
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess && *done == ticket)
                 break;
             if (q != hipErrorNotReady) {
-                HIP_TRY(hipStreamSynchronize(c->stream));
-                if (*done != a.ticket)
+                HIP_TRY(hipStreamSynchronize(stream));
+                if (*done != ticket)
                     return fail(PASTAR_ENODEV, "LDS-resident search ended without its result");
                 break;
             }
         }
     }
-    const double t1 = now_s();
+    return PASTAR_OK;
+}
+
+// The result of an LDS-resident search from its pinned record.
+int solo_finish(pastar_ctx *c, const SearchCfg &cfg, int cap_log2, double seconds, pastar_result *res)
+{
+    int total_len = 0;
+    for (int i = 0; i < c->n; i++)
+        total_len += c->hp.len[i];
+    const size_t C = (size_t)1 << cap_log2;
     SoloOut o;
     std::memcpy(&o, c->h_solo, sizeof(o));
     if (cfg.verbose)
@@ -2069,7 +2108,7 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     h_info[1] = o.path_status;
     c->walk_ready = true;
     c->solo_active = true;
-    c->solo_cap_log2 = pl.a.cap_log2;
+    c->solo_cap_log2 = cap_log2;
     std::memset(res, 0, sizeof(*res));
     res->score = o.score;
     res->expansions = (int64_t)o.expanded;
@@ -2080,7 +2119,7 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     res->closed_size = (int64_t)(o.expanded - o.reopen);
     res->table_used = (int64_t)o.claimed;
     res->steps = o.levels;
-    res->seconds = t1 - t0;
+    res->seconds = seconds;
     res->expand_ms = (double)(o.t_end - o.t_start) * 1e-5;
     res->expand_launches = 1;
     res->expand_parents = (int64_t)(o.expanded + o.dropped);
@@ -2089,6 +2128,26 @@ int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result
     c->searched = true;
     c->score = o.score;
     return PASTAR_OK;
+}
+
+// Returns PASTAR_ENOMEM when the search outgrew the LDS node table (the
+// caller then runs the batched engine).
+int solo_search(pastar_ctx *c, const SearchCfg &cfg, SoloPlan &pl, pastar_result *res)
+{
+    SoloArgs a;
+    volatile uint32_t *done = nullptr;
+    PA_TRY(solo_prepare(c, cfg, pl, &a, &done));
+    const void *fn = solo_fn_for(c->n);
+    if (!(c->solo_attr_done & (1u << c->n))) {
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSoloLds));
+        c->solo_attr_done |= 1u << c->n;
+    }
+    void *args[] = {(void *)&a};
+    const double t0 = now_s();
+    HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(kSoloThreads), args, pl.lds, c->stream));
+    PA_TRY(check_launch());
+    PA_TRY(solo_wait(c->stream, done, a.ticket, t0));
+    return solo_finish(c, cfg, pl.a.cap_log2, now_s() - t0, res);
 }
 
 }  // namespace
@@ -2904,6 +2963,99 @@ int pastar_gpu_selftest_queue(pastar_ctx *c, int scenario, int64_t *info)
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->queues_clean_known = false;  // a cursor without its chunk: clear everything next time
     return check_fault(c);
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Many independent LDS-resident searches in one launch
+// ===========================================================================
+extern "C" {
+
+int pastar_gpu_search_many(pastar_ctx *const *ctxs, int count, const pastar_search_opts *opts, pastar_result *results)
+{
+    if (!ctxs || !results || count < 1 || count > 65535)
+        return fail(PASTAR_EINVAL, "invalid arguments (1..65535 contexts)");
+    pastar_search_opts o{};
+    if (opts)
+        o = *opts;
+    SearchCfg cfg{};
+    cfg.verbose = o.verbose;
+    cfg.band = o.band;
+    cfg.max_steps = o.max_steps;
+    pastar_ctx *c0 = ctxs[0];
+    if (!c0)
+        return fail(PASTAR_EINVAL, "null context");
+    HIP_TRY(hipSetDevice(c0->device));
+    std::vector<SoloArgs> args((size_t)count);
+    size_t lds = 0;
+    const uint64_t stamp = ++g_many_stamp;  // marks the contexts of this call (a context given twice is refused)
+    for (int k = 0; k < count; k++) {
+        pastar_ctx *c = ctxs[k];
+        if (!c)
+            return fail(PASTAR_EINVAL, "null context %d", k);
+        if (c->many_stamp == stamp)
+            return fail(PASTAR_EINVAL, "context %d given twice (each search needs its own result areas)", k);
+        c->many_stamp = stamp;
+        if (c->device != c0->device || c->n != c0->n)
+            return fail(PASTAR_EINVAL, "context %d: every search of one launch runs on one device with one "
+                        "number of sequences (device %d, N = %d)", k, c0->device, c0->n);
+        if (!c->heuristic_ready)
+            return fail(PASTAR_ESTATE, "context %d: pastar_gpu_build_heuristic not called", k);
+        c->walk_ready = false;
+        c->searched = false;
+        c->score = -1;
+        c->lists_ready = false;
+        // a context's launch record is prepared once and reused while its
+        // options stay the same: only the ticket changes
+        if (!c->many_cached || c->many_band != cfg.band || c->many_max_steps != cfg.max_steps) {
+            SoloPlan pl;
+            if (!solo_plan(c, &pl))
+                return fail(PASTAR_EINVAL, "context %d: the problem does not fit the LDS-resident search", k);
+            PA_TRY(solo_prepare(c, cfg, pl, &c->many_a, &c->many_done));
+            c->many_lds = pl.lds;
+            c->many_band = cfg.band;
+            c->many_max_steps = cfg.max_steps;
+            c->many_cached = true;
+        } else {
+            c->many_a.ticket = ++c->solo_ticket;
+            *c->many_done = 0;
+        }
+        args[(size_t)k] = c->many_a;
+        lds = std::max(lds, c->many_lds);
+    }
+    // the argument records, through the first context's staging buffer
+    const size_t bytes = sizeof(SoloArgs) * (size_t)count;
+    if (c0->many_args.n < bytes)
+        PA_TRY(c0->many_args.alloc(bytes));
+    HIP_TRY(hipMemcpyAsync(c0->many_args.p, args.data(), bytes, hipMemcpyHostToDevice, c0->stream));
+    const void *fn = solo_many_fn_for(c0->n);
+    if (!(c0->solo_many_attr_done & (1u << c0->n))) {
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSoloLds));
+        c0->solo_many_attr_done |= 1u << c0->n;
+    }
+    const SoloArgs *dargs = reinterpret_cast<const SoloArgs *>(c0->many_args.p);
+    void *kargs[] = {(void *)&dargs};
+    const double t0 = now_s();
+    HIP_TRY(hipLaunchKernel(fn, dim3((unsigned)count), dim3(kSoloThreads), kargs, lds, c0->stream));
+    PA_TRY(check_launch());
+    // every search reports its own end; the launch's end covers them all
+    HIP_TRY(hipStreamSynchronize(c0->stream));
+    const double seconds = now_s() - t0;
+    int rc = PASTAR_OK;
+    for (int k = 0; k < count; k++) {
+        if (*ctxs[k]->many_done != args[(size_t)k].ticket) {
+            rc = fail(PASTAR_ENODEV, "search %d ended without its result", k);
+            continue;
+        }
+        const int r = solo_finish(ctxs[k], cfg, args[(size_t)k].cap_log2, seconds, &results[k]);
+        if (r != PASTAR_OK) {
+            std::memset(&results[k], 0, sizeof(results[k]));
+            results[k].score = -1;
+            rc = r;
+        }
+    }
+    return rc;
 }
 
 }  // extern "C"

@@ -332,7 +332,7 @@ __device__ __forceinline__ void solo_dump(const SOLO_LDS uint32_t *keys, const S
 typedef solo_v4 SoloEntry;
 
 template <int N>
-__global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
+__device__ __forceinline__ void solo_body(const SoloArgs &a)
 {
     static_assert(N >= 2 && N <= 8, "solo path: 2..8 sequences");
     constexpr int NP = N * (N - 1) / 2;
@@ -1027,6 +1027,22 @@ __global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
     // 4. the node table dump runs on waves 1..3 (solo_dump), beside the
     // result's publication: the host has its answer meanwhile, and
     // pastar_gpu_closed_lookup's kernel is stream-ordered after this one
+}
+
+template <int N>
+__global__ __launch_bounds__(kSoloThreads, 1) void solo_kernel(SoloArgs a)
+{
+    solo_body<N>(a);
+}
+
+// Many independent searches in one launch: workgroup b runs the search
+// args[b] describes (its own problem, LDS layout, result areas), each whole
+// in its CU's LDS as above.  The workgroups share nothing.
+template <int N>
+__global__ __launch_bounds__(kSoloThreads, 1) void solo_many_kernel(const SoloArgs *__restrict__ args)
+{
+    const SoloArgs a = args[blockIdx.x];
+    solo_body<N>(a);
 }
 
 // Closed-list lookup in a solo search's dumped node table (kernels.hpp

@@ -386,6 +386,23 @@ class Engine:
         return [raw[i * stride:i * stride + n].decode("latin-1") for i in range(self.n)]
 
 
+def search_many(engines, opt=None):
+    """pastar_gpu_search_many: the searches of `engines` (one problem each,
+    small enough for the LDS-resident engine, same device and number of
+    sequences) in one launch.  Returns their SearchResults; each engine then
+    answers alignment() for its own search."""
+    opt = opt or PAStarOpt()
+    for e in engines:
+        if not e._ready:
+            e.init()
+    k = len(engines)
+    arr = (ctypes.c_void_p * k)(*[e._ctx.value for e in engines])
+    res = (nat.pastar_result * k)()
+    so = opt.search_opts()
+    check(lib().pastar_gpu_search_many(arr, k, ctypes.byref(so), res))
+    return [SearchResult(*r.as_tuple()) for r in res]
+
+
 def _c_nodes(nodes):
     arr = (nat.pastar_node * max(len(nodes), 1))()
     for k, nd in enumerate(nodes):

@@ -183,3 +183,45 @@ def test_solo_long_paths(length, mutate):
             assert rows == seqs
         rb = e.pa_star(PAStarOpt(mode="batched"))
         assert rb.score == r.score and e.alignment() == rows
+
+
+def test_search_many_matches_single_searches(kat):
+    """pastar_gpu_search_many: independent searches of different problems
+    (same N) in one launch, one workgroup each, against the same searches run
+    one by one and against the oracle: scores, expansion counts, alignments."""
+    import random
+    from mpi_pastar_msa_amd import search_many
+    rng = random.Random(5)
+    ref = kat["inputs"]["PF08184"]
+    problems = [Sequences.from_fasta(golden(ref["file"]))]
+    for _ in range(9):
+        root = [rng.choice("ACDEFGHIKLMNPQRSTVWY") for _ in range(rng.randint(20, 50))]
+        seqs = []
+        for _ in range(3):
+            s = [rng.choice("ACDEFGHIKLMNPQRSTVWY") if rng.random() < 0.15 else c for c in root if rng.random() > 0.05]
+            seqs.append("".join(s) or "A")
+        problems.append(Sequences(seqs))
+    engines = [Engine(p).init() for p in problems]
+    try:
+        many = search_many(engines)
+        rows_many = [e.alignment() for e in engines]
+        for p, e, r, rows in zip(problems, engines, many, rows_many):
+            o = orc.Oracle(seqs=p.seqs)
+            want = o.astar()
+            assert r.solo == 1 and r.score == want["score"]
+            assert o.alignment_cost(rows) == r.score
+            assert [row.replace("-", "") for row in rows] == p.seqs
+            single = e.pa_star(PAStarOpt(mode="solo"))
+            assert (single.score, single.expansions_all, single.generated) == (r.score, r.expansions_all, r.generated)
+            assert e.alignment() == rows
+        assert many[0].score == ref["score"] and many[0].expansions_all == ref["expansions_t1"]
+        # the same batch again (the contexts' result areas are reused), and a
+        # batch that repeats a context is refused
+        again = search_many(engines)
+        assert [r.score for r in again] == [r.score for r in many]
+        with pytest.raises(NativeError) as ei:
+            search_many([engines[0], engines[0]])
+        assert ei.value.code == EINVAL
+    finally:
+        for e in engines:
+            e.close()
