@@ -2193,8 +2193,10 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     // search then runs without a capacity restart; tools/gpu/cold_probe.py)
     // (an explicit size is a floor: a repeated search never restarts below
     // what the last one needed)
+    // (N >= 7: 2^26, 2 GB: syn8x400's first search ran 164 ms with a
+    // capacity restart from 2^24 against 73 ms warm)
     cfg.table_log2 = o.table_slots_log2 > 0 ? std::max((int)o.table_slots_log2, c->learned_log2)
-                                            : (c->learned_log2 > 0 ? c->learned_log2 : 24);
+                                            : (c->learned_log2 > 0 ? c->learned_log2 : (c->n >= 7 ? 26 : 24));
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
         return fail(PASTAR_EINVAL, "table_slots_log2 %d outside [10, 32]", cfg.table_log2);
     // (the pool is never cleared: its size costs memory only, 2 GB here)

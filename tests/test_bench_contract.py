@@ -33,7 +33,14 @@ def test_cpu_baseline_schema():
     runs = line["runs"]
     assert "t1" in runs and len(runs) == 2
     assert runs["t1"]["cores"] == 1
-    assert line["value"] == max(r["value"] for r in runs.values())
+    # the baseline is the leg that reaches the optimum sooner, not the one with more nodes/s
+    assert line["wall_to_optimal_s"] == min(r["wall_to_optimal_s"] for r in runs.values())
+    assert line["chosen_by"] == "wall_to_optimal_s"
+
+
+def test_sharded_shift_choice():
+    assert bench.sharded_shift(5, 1) == 12 and bench.sharded_shift(8, 1) == 12
+    assert bench.sharded_shift(4, 8) == 18 and bench.sharded_shift(5, 2) == 18 and bench.sharded_shift(8, 8) == 12
 
 
 def test_cpu_baseline_rejects_a_wrong_score():
