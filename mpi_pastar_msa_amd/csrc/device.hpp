@@ -313,7 +313,6 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
     else
         idx = probe_start<KW>(key, cap_mask);
     int probe = 0;
-    unsigned tail_polls = 0;
     // the prefetched slots: skip those holding other keys (key word 0 set
     // and different), and start at the first empty or candidate one with
     // its prefetched words (constant indices only: no register array is
@@ -388,22 +387,22 @@ __device__ __forceinline__ int64_t relax(uint64_t *__restrict__ table, uint64_t 
                 probe++;
                 continue;
             }
-            bool same = true, pending = false;
+            bool same = true;
 #pragma unroll
             for (int w = 1; w < KW; w++) {
                 uint64_t v = wv[w];
-                if (v == 0)
-                    v = __hip_atomic_load(s + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                pending |= (v == 0);
+                if (v == 0) {
+                    // unknown, or still being published by a claimant that
+                    // is past its CAS and stores the tail next: read it, a
+                    // bounded number of times (the counter lives only here)
+                    unsigned poll = 0;
+                    do
+                        v = __hip_atomic_load(s + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    while (v == 0 && ++poll < kSpinLimit);
+                    if (v == 0)
+                        return -2;
+                }
                 same &= (v == key[w]);
-            }
-            if (pending) {
-                // tail still being published (by a claimant that is past its
-                // CAS and stores the tail next): re-read this slot, a bounded
-                // number of times
-                if (++tail_polls > kSpinLimit)
-                    return -2;
-                continue;
             }
             if (!same) {
                 idx = (idx + 1) & cap_mask;

@@ -495,6 +495,13 @@ struct Ctl {
     unsigned long long blk_stats[10];
     int dbg_hits, dbg_bucket, dbg_cur, dbg_win, dbg_step;
     int fault_sites;  // status 4: the kSite* bits select found in the fault word
+    // kSite* bits of bounded device waits that ran out (device.hpp), ORed in
+    // by the waiter: sticky, kept across the per-search upload of this block
+    // (search_init_kernel skips the word), cleared by the host when it
+    // reports the fault.  The PairAlign kernel, which runs before a search's
+    // setup, flags its band wait here too.
+    alignas(128) int fault;
+    unsigned spin_limit;  // polls a queue store waits for its chunk id (kSpinLimit; tests lower it)
     unsigned long long dbg_w, dbg_r;
 };
 
@@ -526,14 +533,16 @@ constexpr int kMaxExpandBlocks = 4096;
 // register budget of expand_kernel<N, KW>: waves per SIMD it must fit, which
 // is also its resident blocks per CU (a block is one wave on each SIMD)
 // (5 for N <= 5 spills 36-72 B per lane and ran kinase 20% slower)
-__host__ __device__ constexpr int expand_waves_per_eu(int, int) { return 4; }
+#ifndef PASTAR_WIDE_WAVES
+#define PASTAR_WIDE_WAVES 4
+#endif
+__host__ __device__ constexpr int expand_waves_per_eu(int n, int) { return n >= 7 ? PASTAR_WIDE_WAVES : 4; }
 constexpr int kTraceSteps = 4096;
 
 struct SearchArgs {
     const DevProblem *P;
-    Ctl *ctl;
-    int *fault;           // kSite* bits of waits that ran out (sticky until the host clears it)
-    unsigned spin_limit;  // polls a queue store waits for its chunk id (kSpinLimit; tests lower it)
+    Ctl *ctl;  // (also holds the fault word and the store wait's poll limit: values the hot loops never
+               // touch stay out of the kernel arguments, which live in scalar registers for the whole launch)
     unsigned long long *stamps;  // [kArrive] start stamps of the first blocks
     int *trace;                  // debug: [kTraceSteps][8] per-step select trace (nullptr: off)
     uint64_t *table;
@@ -637,11 +646,19 @@ __device__ __forceinline__ int bucket_of(int f, int f0, int w)
 __device__ __forceinline__ unsigned long long queue_reserve(const SearchArgs &a, int b, int sq, unsigned n)
 {
     const unsigned long long base = atomicAdd(&a.q->W[b][sq], (unsigned long long)n);
-    for (unsigned long long k = (base + kChunk - 1) >> kChunkLog2; (k << kChunkLog2) < base + n && k < a.maxch; k++) {
-        const unsigned long long id = atomicAdd(&a.ctl->pool_top, 1ull);
-        const uint32_t c = id < a.pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
-        __hip_atomic_store(a.chunk_tab + ((size_t)b * kSub + sq) * a.maxch + k, c, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    // (n <= kChunk: at most one chunk starts inside the range; the rare
+    // path reads its capacities from the control block, not from kernel
+    // arguments that would sit in scalar registers for the whole launch)
+    const unsigned to_next = (unsigned)(-(long long)base) & (kChunk - 1);  // positions up to the next chunk start
+    if (to_next < n) {
+        const unsigned long long k = (base + to_next) >> kChunkLog2;
+        Ctl *ctl = a.ctl;
+        if (k < a.maxch) {
+            const unsigned long long id = atomicAdd(&ctl->pool_top, 1ull);
+            const uint32_t c = id < ctl->pool_chunks ? (uint32_t)(id + 1) : kNoChunk;
+            __hip_atomic_store(a.chunk_tab + ((size_t)b * kSub + sq) * a.maxch + k, c, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     return base;
 }
@@ -663,12 +680,13 @@ __device__ __forceinline__ void queue_store(const SearchArgs &a, int b, int sq, 
     uint32_t *tp = a.chunk_tab + ((size_t)b * kSub + sq) * maxch + k;
     uint32_t c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (c == 0) {
-        for (unsigned poll = 0; poll < a.spin_limit && c == 0; poll++) {
+        const unsigned limit = a.ctl->spin_limit;
+        for (unsigned poll = 0; poll < limit && c == 0; poll++) {
             __builtin_amdgcn_s_sleep(1);
             c = __hip_atomic_load(tp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (c == 0) {  // the wait ran out: flag it, drop the entry
-            atomicOr(a.fault, (int)kSiteQueueStore);
+            atomicOr(&a.ctl->fault, (int)kSiteQueueStore);
             return;
         }
     }
@@ -790,7 +808,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
         slot = relax<KW, PFS>(a.table, a.cap_mask, ck, g, m, h, improved, cl, has_pre, pre, &lowered);
         if (slot < 0) {
             if (slot == -2)
-                atomicOr(a.fault, (int)kSiteRelaxTail);
+                atomicOr(&a.ctl->fault, (int)kSiteRelaxTail);
             ovf++;
             improved = false;
             lowered = false;
@@ -902,7 +920,10 @@ __device__ __forceinline__ SelView load_view(const Ctl *ctl)
     return v;
 }
 
-// Requires ctl->status == 0 on entry.
+// Requires ctl->status == 0 on entry.  X: the sharded search (a.x set): its
+// window, backpressure and insert-side counters compile out of the one-shard
+// search's fused select.
+template <bool X>
 __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView &v)
 {
     Ctl *ctl = a.ctl;
@@ -971,11 +992,11 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         found = kBuckets;
         found2 = kBuckets;
     } else if (tid == kStatRows + 6) {
-        fault_s = ld_agent(a.fault);
+        fault_s = ld_agent(&ctl->fault);
     } else if (tid == kStatRows + 7) {
         low_s = ld_agent(&ctl->low_b) < kBuckets ? atomicExch(&ctl->low_b, kBuckets) : kBuckets;
-        claimed_b_s = a.x ? a.x->claimed_b : 0;
-        gmin_s = a.x ? ld_agent(&a.x->gmin_b) : kBuckets;
+        claimed_b_s = X ? a.x->claimed_b : 0;
+        gmin_s = X ? ld_agent(&a.x->gmin_b) : kBuckets;
     }
     __syncthreads();
     PHASE(0)
@@ -1009,8 +1030,8 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
     // again once the cheaper paths through the other shards' lower buckets
     // arrive (syn8x400 at 8 shards: 27-46 M expansions for 5.8 M without
     // the window).  limit still decides whether the shard has work at all.
-    const int xwin = ctl->xwindow;
-    const int limit_take = (gmin_s < kBuckets && gmin_s + xwin - 1 < limit) ? gmin_s + xwin - 1 : limit;
+    const int xwin = X ? ctl->xwindow : kBuckets;
+    const int limit_take = (X && gmin_s < kBuckets && gmin_s + xwin - 1 < limit) ? gmin_s + xwin - 1 : limit;
     const int start_c = cur_s < b_win ? cur_s : b_win;
     const int start = low_s < start_c ? low_s : start_c;
     if (start == b_win) {
@@ -1142,7 +1163,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         const int k = (2 * tid) / kSub;                       // bucket offset of both ranges
         const unsigned long long bstart = __shfl(ex0, k * (kSub / 2));  // entries before bucket k
         // (sharded: a shard holds about 1 / n_shards of a thin bucket)
-        const unsigned long long kmin = a.x ? v.kmin / (unsigned long long)ctl->n_shards : v.kmin;
+        const unsigned long long kmin = X ? v.kmin / (unsigned long long)ctl->n_shards : v.kmin;
         const bool incl = k == 0 || bstart < kmin;
         const int n_incl = __popcll(__ballot(incl && (tid % (kSub / 2)) == 0 && b + k <= limit_take));
         // sharded: no more parents than the outbox rings can take children
@@ -1151,7 +1172,7 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         // a parent can have (an overflow past this estimate restarts the
         // search with larger rings)
         unsigned long long kmax = v.kmax;
-        if (a.x && ctl->n_shards > 1) {
+        if (X && ctl->n_shards > 1) {
             unsigned long long free_min = ~0ull;
             for (int d = 0; d < ctl->n_shards; d++) {
                 if (d == a.P->shard)
@@ -1198,8 +1219,12 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
 
 __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
 {
-    if (!a.ctl->status)
-        select_block(a, load_view(a.ctl));
+    if (!a.ctl->status) {
+        if (a.x)
+            select_block<true>(a, load_view(a.ctl));
+        else
+            select_block<false>(a, load_view(a.ctl));
+    }
     if (!a.x)
         return;
     // Sharded search: what this shard tells the others about step a.step,
@@ -1224,7 +1249,7 @@ __global__ __launch_bounds__(kBlock) void select_kernel(SearchArgs a)
         else if (status == 4)
             fl |= 0x200;
         fl |= ld_agent(&a.x->fail_b);  // the insert kernel's overflows (folded by the pack kernel)
-        if (ld_agent(a.fault))
+        if (ld_agent(&ctl->fault))
             fl |= 0x200;
         si.fail = fl;
         a.x->info[a.step & (kXSlots - 1)] = si;
@@ -1939,7 +1964,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     }
     const unsigned long long ts = timing ? device_clock() : 0;
     if (fuse)
-        select_block(a, view);
+        select_block<false>(a, view);  // (the sharded search selects in its own launch)
     if (timing && threadIdx.x == 0) {
         const unsigned long long t1 = device_clock();
         if (t1 > t0) {
@@ -2016,7 +2041,6 @@ struct XArgs {
     Ctl *ctl;
     StepStats *stats_b;  // the insert kernel's own step statistics
     const int *goal_g;
-    const int *fault;
     void *outbox;        // Remote<KW>[n_shards][outbox_cap] rings
     unsigned long long outbox_cap;
     unsigned char *send;  // [n_shards] blocks of block_bytes
@@ -2183,7 +2207,7 @@ __global__ __launch_bounds__(kBlock) void xinsert_kernel(SearchArgs a, XArgs t)
                 // a shard failed: every shard stops at this step (each
                 // reports its own fail bits; 0x200: a device wait ran out)
                 if (fl & 0x200) {
-                    ctl->fault_sites = *t.fault;
+                    ctl->fault_sites = ld_agent(&ctl->fault);
                     ctl->status = 4;
                 } else if (fl & 0x100) {
                     ctl->status = 3;
@@ -2321,7 +2345,8 @@ __global__ __launch_bounds__(kBlock) void search_init_kernel(uint64_t *__restric
         if (seed_taken && !reset_queues && threadIdx.x == 0)
             q->R[0][0] = 1;  // (the queues were cleared by a memset)
         for (int k = threadIdx.x; k < stage_words; k += blockDim.x)
-            ctl_dst[k] = stage[k];
+            if (k != (int)(offsetof(Ctl, fault) / 4))  // (sticky: see Ctl::fault)
+                ctl_dst[k] = stage[k];
         unsigned long long *sw = reinterpret_cast<unsigned long long *>(stats);
         for (int k = threadIdx.x; k < (int)(sizeof(StepStats) / 8); k += blockDim.x)
             sw[k] = 0;

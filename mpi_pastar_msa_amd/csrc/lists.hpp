@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kListThreads) void lists_enqueue_kernel(SearchArgs 
                             SlotWords<KW, 1>{});
         if (slot < 0) {
             if (slot == -2)
-                atomicOr(a.fault, (int)kSiteRelaxTail);
+                atomicOr(&a.ctl->fault, (int)kSiteRelaxTail);
             improved = false;
             atomicAdd(&out[1], 1ull);
         } else if (improved) {

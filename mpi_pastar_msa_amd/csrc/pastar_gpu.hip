@@ -267,8 +267,7 @@ struct pastar_ctx {
     std::unique_ptr<Transport> tr;
     DevBuf<int64_t> xred;           // RCCL staging of small collectives
     unsigned char *scratch = nullptr;  // this device's copy of the static scratch array (hipGetSymbolAddress)
-    DevBuf<int> fault;              // kSite* bits of bounded device waits that ran out (kernels.hpp)
-    unsigned spin_limit = kSpinLimit;
+    unsigned spin_limit = kSpinLimit;  // (the fault word of bounded device waits is Ctl::fault)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // sharded search: the side stream of the record exchange and the event
@@ -543,7 +542,7 @@ const char *fault_site_name(int sites)
 // word: report it as PASTAR_EDEVWAIT and clear the word (the stream is idle).
 int report_fault(pastar_ctx *c, int sites)
 {
-    (void)hipMemset(c->fault.p, 0, sizeof(int));
+    (void)hipMemset(&c->ctl.p->fault, 0, sizeof(int));
     return fail(PASTAR_EDEVWAIT, "a device wait ran out of its bound at: %s (sites 0x%x); results discarded",
                 fault_site_name(sites), sites);
 }
@@ -553,7 +552,7 @@ int report_fault(pastar_ctx *c, int sites)
 int check_fault(pastar_ctx *c)
 {
     int sites = 0;
-    HIP_TRY(hipMemcpy(&sites, c->fault.p, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&sites, &c->ctl.p->fault, sizeof(int), hipMemcpyDeviceToHost));
     return sites ? report_fault(c, sites) : PASTAR_OK;
 }
 
@@ -767,8 +766,11 @@ int pastar_gpu_create(const pastar_problem *p, int device, int n_shards, int sha
     HIP_TRY(hipEventCreate(&c->ev0));
     HIP_TRY(hipEventCreate(&c->ev1));
     PA_TRY(setup_problem(c.get(), p));
-    PA_TRY(c->fault.alloc(1));
-    HIP_TRY(hipMemset(c->fault.p, 0, sizeof(int)));
+    // the control block (and the search's origin record behind it) exists
+    // from the start: it holds the fault word every kernel with a bounded
+    // wait reports to
+    PA_TRY(c->ctl.alloc(2));
+    HIP_TRY(hipMemset(c->ctl.p, 0, 2 * sizeof(Ctl)));
     // each GPU holds its own copy of the scratch array at its own address:
     // resolved here, with this context's device current
     HIP_TRY(hipGetSymbolAddress((void **)&c->scratch, HIP_SYMBOL(scratch)));
@@ -875,7 +877,8 @@ static int launch_pairalign(pastar_ctx *c, bool write_h)
                                  : (const void *)pairalign_wave_kernel<false, false, false>));
     if (lds > 64 * 1024)
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p, (void *)&c->fault.p, (void *)&c->spin_limit};
+    int *fault = &c->ctl.p->fault;
+    void *args[] = {(void *)&c->dP.p, (void *)&c->dH.p, (void *)&c->dHC.p, (void *)&fault, (void *)&c->spin_limit};
     HIP_TRY(hipLaunchKernel(fn, dim3(c->npairs), dim3(64 * kPaWaves), args, lds, c->stream));
     PA_TRY(check_launch());
     // the search and h run on the same stream, so the search-form tables
@@ -1130,7 +1133,6 @@ int alloc_search(pastar_ctx *c, const SearchCfg &cfg)
     if (!c->queues.p) {
         PA_TRY(c->queues.alloc(1));
         PA_TRY(c->stats.alloc(1));
-        PA_TRY(c->ctl.alloc(2));  // the Ctl, then the search's origin record (one upload)
         PA_TRY(c->stamps.alloc(kArrive));
         PA_TRY(c->goal.alloc(1));
         c->queues_clean_known = false;
@@ -1359,6 +1361,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
+    hc.spin_limit = c->spin_limit;
     hc.low_b = kBuckets;
     // (kinase at 8 shards: 147 steps at 4 buckets, 124 at 8; syn8x400: 10.9 M
     // expansions at 4, 19 M at 8; tools/gpu/probe_shards.py)
@@ -1392,8 +1395,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     SearchArgs a{};
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
-    a.fault = c->fault.p;
-    a.spin_limit = c->spin_limit;
     a.stamps = c->stamps.p;
     DevBuf<int> trace;
     a.trace = nullptr;
@@ -1670,7 +1671,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         t.ctl = c->ctl.p;
         t.stats_b = c->stats_b.p;
         t.goal_g = c->goal.p;
-        t.fault = c->fault.p;
         t.outbox = c->outbox.p;
         t.outbox_cap = cfg.outbox_cap;
         t.recv = c->xrecv.p;
@@ -2697,6 +2697,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     hc.table_slots = c->nslots;
     hc.cur_b = kBuckets;  // empty: appends lower it
     hc.low_b = kBuckets;
+    hc.spin_limit = c->spin_limit;
     std::memcpy(c->h_stage, &hc, sizeof(Ctl));
     PA_TRY(init_search(c, cfg, sizeof(Ctl)));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2704,8 +2705,6 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     a = SearchArgs{};
     a.P = c->dP.p;
     a.ctl = c->ctl.p;
-    a.fault = c->fault.p;
-    a.spin_limit = c->spin_limit;
     a.stamps = c->stamps.p;
     a.table = c->table.p;
     a.cap_mask = c->nslots - 1;
@@ -2761,7 +2760,7 @@ int pastar_gpu_open_enqueue(pastar_ctx *c, const pastar_node *nodes, int count, 
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_flags, dflags, fb, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_res, dres, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 16, &c->stats.p->ovf_near, 16, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 32, c->fault.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_lists + off_res + 32, &c->ctl.p->fault, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const unsigned long long *r = reinterpret_cast<const unsigned long long *>(c->h_lists + off_res);
     if (const int sites = *reinterpret_cast<const int *>(c->h_lists + off_res + 32)) {
@@ -2959,7 +2958,8 @@ int pastar_gpu_selftest_queue(pastar_ctx *c, int scenario, int64_t *info)
     // call must report PASTAR_EDEVWAIT
     const unsigned long long lost = 8;
     HIP_TRY(hipMemcpyAsync(&c->queues.p->W.d[0][b1], &lost, sizeof(lost), hipMemcpyHostToDevice, c->stream));
-    a.spin_limit = 64;
+    const unsigned few = 64;
+    HIP_TRY(hipMemcpyAsync(&c->ctl.p->spin_limit, &few, sizeof(few), hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(selftest_lost_opener_kernel, dim3(1), dim3(64), 0, c->stream, a, b1);
     PA_TRY(check_launch());
     HIP_TRY(hipStreamSynchronize(c->stream));

@@ -25,7 +25,7 @@ __device__ __forceinline__ void selftest_wait(const SearchArgs &a, unsigned *fla
             return;
         __builtin_amdgcn_s_sleep(4);
     }
-    atomicOr(a.fault, (int)kSiteSelftest);
+    atomicOr(&a.ctl->fault, (int)kSiteSelftest);
 }
 
 // Crossed reservations.  Two workgroups X (block 0) and Z (block 1) append
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(64) void selftest_crossed_check_kernel(SearchArgs a
 // A store into a chunk nobody opened: the host has moved sub-queue (b, 0)'s
 // cursor to `lost` (> 0, inside chunk 0) without opening the chunk, as if a
 // reserver had vanished between its cursor add and its publication.  The
-// stores wait a.spin_limit polls (set low by the host), flag the fault word
+// stores wait Ctl::spin_limit polls (set low by the host), flag the fault word
 // and drop their entries; the kernel ends.
 __global__ __launch_bounds__(64) void selftest_lost_opener_kernel(SearchArgs a, int b)
 {
