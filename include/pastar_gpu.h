@@ -128,7 +128,15 @@ typedef struct pastar_search_opts {
                                  the owner's insert of step i run beside the
                                  expansion of step i + 1 (side stream), and
                                  their records reach the select after        */
-    int32_t pad0;
+    int32_t partial;          /* partial expansion (PEA*: a parent's children
+                                 whose f lies at or past a window beyond the
+                                 step's buckets are generated only when the
+                                 parent comes up again, queued under the
+                                 lowest f among them; results are the same,
+                                 most of a wide fan-out is never probed):
+                                 0 = default (on for N >= 7, window of one
+                                 bucket), n > 0: window of n - 1 buckets,
+                                 -1: off; ignored for N <= 6               */
     int64_t xchg_block_records; /* most records one step carries to one shard
                                  (the all-to-all's block, a power of two of
                                  records sized per round from the demand seen,

@@ -57,7 +57,7 @@ class pastar_search_opts(ctypes.Structure):
         ("depth", ctypes.c_int32),
         ("mode", ctypes.c_int32),
         ("xchg_lag", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
+        ("partial", ctypes.c_int32),
         ("xchg_block_records", ctypes.c_int64),
     ]
 

@@ -96,17 +96,25 @@ struct Entry {  // open-pile entry
     uint32_t slot;
     int32_t f;
 };
+// Partial expansion (search kernels): a parent whose children at or past a
+// cutoff were left ungenerated goes back to the open list under the lowest f
+// among them, marked by the sign bit of f (f itself is never negative: costs
+// and h are sums of non-negative terms).  Taken again, it generates the
+// children from that f on, under the node's best g at that time.
+constexpr int32_t kPartialBit = (int32_t)0x80000000;
+__host__ __device__ inline int32_t entry_f(const Entry &e) { return e.f & 0x7fffffff; }
 
 // Per-step counters.  The counters every wave adds to are spread over
 // kStatRows rows (row = global wave index % kStatRows): a single word takes
 // one atomic per wave and saturates at ~88 atomics/us, which at 5-10 K waves
 // per step would serialise for 50-100 us; select sums the rows.
 constexpr int kStatRows = 64;
-enum { kStExpanded, kStReopen, kStGenerated, kStClaimed, kStDropped, kStOvfTable, kStFields = 8 };
+enum { kStExpanded, kStReopen, kStGenerated, kStClaimed, kStDropped, kStOvfTable, kStPartQueued, kStPartTaken, kStFields = 8 };
 struct StepStats {
     // expanded: parents that passed the stale/closed checks; reopen; generated:
     // border-valid children; claimed: new table slots; dropped: stale or
-    // pruned parents; ovf_table: node table probe limit hit
+    // pruned parents; ovf_table: node table probe limit hit; part_queued /
+    // part_taken: parents queued again with children left, and taken again
     unsigned long long row[kStatRows][2 * kStFields];  // one 128-B line per row
     unsigned long long ovf_near;  // chunk pool exhausted
     unsigned long long ovf_far;   // sub-queue chunk table exhausted

@@ -459,6 +459,11 @@ struct Ctl {
     int xwindow;    // sharded: buckets above the shards' common lowest live bucket a batch may be cut from
     int debug;      // 1: select validates its scan start (diagnostics)
     int deep_blocks;  // block-rounds per continuation level across the chip (kDeepBlocks by default)
+    int prune_f;      // children with f >= this are not generated (an upper bound of the optimum + 1; kIntMax: none)
+    int partial_k;    // partial expansion: children with f at or past the batch's last bucket + this many buckets
+                      // wait until their parent is taken again (negative: every child at once)
+    int partial_ahead;  // that parent is queued this many buckets before its first waiting child's
+    int partial_two;    // 1: a parent taken again generates every child it has left
     unsigned long long kmax;
     unsigned long long pool_chunks, maxch;
     unsigned long long table_slots;
@@ -468,6 +473,7 @@ struct Ctl {
     // ---- select's running totals ----
     long long steps, max_steps;
     unsigned long long expanded, reopen, generated, claimed, dropped, parents;
+    unsigned long long part_queued, part_taken;  // partial expansion: parents queued again / taken again
     // ---- atomics, one line each ----
     alignas(128) unsigned long long pool_top;  // chunk bump allocator
     alignas(128) int cur_b;  // lowest bucket that may hold entries (f_min only grows)
@@ -779,6 +785,35 @@ __device__ __forceinline__ int group_verdict(int verdict, int leader_lane)
 // queue entries) need not land before the block moves on.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Open-list append of the predicated lanes' entries: into the block's
+// deferred buffer while it has room (one cursor atomic per bucket for the
+// whole block at the end of the launch), else at once.  Every lane of the
+// wave must call it.
+template <int KW>
+__device__ __forceinline__ void open_append(const SearchArgs &a, const LocalPush<KW> &lp, bool pred, int b,
+                                            const Entry &e, StepStats *st, bool may_lower)
+{
+    if (lp.out) {
+        const uint64_t mask = __ballot(pred);
+        if (mask) {
+            const int lane = lane_id();
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader)
+                base = atomicAdd(lp.out_n, __popcll(mask));
+            base = bcast_lane(base, leader);
+            if (pred) {
+                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (pos < kOutCap) {
+                    lp.out[pos] = e;
+                    pred = false;
+                }
+            }
+        }
+    }
+    queue_append(a, pred, b, e, st, may_lower);
+}
+
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
 // All lanes of the wave must call it.
@@ -853,25 +888,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
             }
         }
     }
-    if (lp.out) {  // defer to the block's final append (one atomic per bucket and wave there)
-        const uint64_t mask = __ballot(global);
-        if (mask) {
-            const int lane = lane_id();
-            const int leader = __ffsll((long long)mask) - 1;
-            int base = 0;
-            if (lane == leader)
-                base = atomicAdd(lp.out_n, __popcll(mask));
-            base = bcast_lane(base, leader);
-            if (global) {
-                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-                if (pos < kOutCap) {
-                    lp.out[pos] = e;
-                    global = false;
-                }
-            }
-        }
-    }
-    queue_append(a, global, bucket_of(f, f0, w), e, st, remote_in);
+    open_append(a, lp, global, bucket_of(f, f0, w), e, st, remote_in);
     if (SH && P.n_shards > 1) {
         const bool remote = valid && !local && lowered;
         Remote<KW> rec;
@@ -1007,6 +1024,10 @@ __device__ __forceinline__ void select_block(const SearchArgs &a, const SelView 
         ctl->generated = acc[2] + sums[kStGenerated];
         ctl->claimed = claimed;
         ctl->dropped = acc[4] + sums[kStDropped];
+        if (sums[kStPartQueued] | sums[kStPartTaken]) {  // (partial expansion only: read-modify-write off the common path)
+            ctl->part_queued += sums[kStPartQueued];
+            ctl->part_taken += sums[kStPartTaken];
+        }
         ctl->parents = acc[5] + v.n_batch;
         int fm = fail_bits(ovf[0], ovf[1], sums[kStOvfTable], ovf[2]);
         if ((claimed + claimed_b_s) * 10 > v.table_slots * 7)
@@ -1404,10 +1425,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
 #endif
     StepStats *st = a.stats;
     const int w = view.band_log2, f0 = view.f0;
-    const int bound = *(volatile int *)a.goal_g;
+    const int goal_now = *(volatile int *)a.goal_g, prune_f = ctl->prune_f;
+    const int bound = goal_now < prune_f ? goal_now : prune_f;
     // per-lane statistics of one launch (32-bit: at most a few million)
-    unsigned expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0;
+    unsigned expanded = 0, reopen = 0, generated = 0, claimed = 0, ovf = 0, stale = 0, part_q = 0, part_t = 0;
     const int masks = 1 << n;
+    // upper edge of the batch's buckets: improved children below it continue
+    // in this launch (block-local continuation)
+    const int f_limit = f0 + (int)(((long long)view.batch_b + view.batch_nb) << w);
+    // partial expansion (wide fan-outs: several child rounds per parent): a
+    // child with f at or past `cutoff` is not generated now; its parent goes
+    // back to the open list under the lowest such f and generates the rest
+    // when it is taken again.  Most parents are expanded in the search's last
+    // buckets, and their costlier children never come up before the search
+    // ends: no probe, no table slot, no queue entry for them.  (A batch that
+    // reaches the last bucket, which also holds everything above, expands in
+    // full: the re-queued parent must land past its batch.)
+    constexpr bool kPartial = N == 0 || N >= 7;
+    const int partial_k = kPartial ? ctl->partial_k : -1;
+    const int partial_ahead = kPartial ? ctl->partial_ahead : 0;
+    const int partial_two = kPartial ? ctl->partial_two : 0;
+    const int cutoff = (partial_k >= 0 && view.batch_b + view.batch_nb + partial_k < kBuckets - 1)
+                           ? f_limit + (int)((long long)partial_k << w)
+                           : kIntMax;
     __syncthreads();
     BPHASE(0)
     // expand one parent per lane group: entry -> staleness / closed check ->
@@ -1425,6 +1465,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         for (int k = 0; k < KW; k++)
             par_.key[k] = 0;
         uint64_t lbest = 0, laux = 0;
+        int resume = 0;            // partial expansion: children below this f were generated before
+        int pend_f = kIntMax;      // lowest f among the children left for later
+        int cut = cutoff;          // (a parent taken again generates all it has left: at most two passes)
         if (ok && local) {
 #pragma unroll
             for (int k = 0; k < KW; k++)
@@ -1447,20 +1490,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             const int h = (int)(aux >> 32);
             par_.g = (int)(best >> 32);
             par_.pmask = (int)(uint32_t)best;
-            // an entry is current iff its f is the node's f under the best g
-            // found so far; improvements are strict, so a current entry is
-            // unique and the closed mark needs no atomic
-            ok = (par_.g + h == e.f) && e.f < bound;
-            int verdict = ok ? 1 : 0;
-            if (ok && glane == 0) {
-                int *closed = (int *)(a.table + (uint64_t)e.slot * SW + KW + 1);
-                verdict = (int)(uint32_t)aux != kIntMax ? 2 : 1;
-                *closed = par_.g;
+            const bool part = kPartial && e.f < 0;
+            const int ef = entry_f(e);
+            int verdict;
+            if (part) {
+                // the rest of a partially expanded parent, generated under
+                // the node's best g as of now; not a new expansion.  Always
+                // current: had the node improved since it was queued, the
+                // improvement's own entry expands it from the start (and
+                // queues its own rest), so this one only repeats part of
+                // that; nothing tells the two apart cheaply, and nothing
+                // needs to (relaxations are idempotent)
+                verdict = ef < bound ? 1 : 0;
+                resume = ef;
+                if (partial_two == 1)
+                    cut = kIntMax;
+                else if (partial_two == 2 && cutoff != kIntMax) {
+                    // each pass reaches as far past the batch as the last one
+                    // left off past the parent's own f
+                    const long long far = (long long)f_limit + (ef - (par_.g + h));
+                    cut = far > cutoff ? (far < kIntMax ? (int)far : kIntMax) : cutoff;
+                }
+            } else {
+                // an entry is current iff its f is the node's f under the
+                // best g found so far; improvements are strict, so a current
+                // entry is unique and the closed mark needs no atomic
+                verdict = ((par_.g + h == ef) && ef < bound) ? 1 : 0;
+                if (verdict && glane == 0) {
+                    int *closed = (int *)(a.table + (uint64_t)e.slot * SW + KW + 1);
+                    verdict = (int)(uint32_t)aux != kIntMax ? 2 : 1;
+                    *closed = par_.g;
+                }
             }
             verdict = group_verdict(verdict, leader_lane);
             ok = verdict != 0;
             if (glane == 0) {
-                expanded += ok;
+                expanded += ok && !part;
+                part_t += ok && part;
                 reopen += verdict == 2;
                 stale += !ok;
             }
@@ -1538,9 +1604,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 const int2 dc = child_cost<N>(Pg, npairs, terms, m);
                 g = par_.g + dc.x;
                 h = dc.y;
-                generated++;
-                if (g + h >= bound)
+                const int f = g + h;
+                if (kPartial && (f < resume || f >= cut)) {
                     valid = false;
+                    if (f >= cut && f < bound)
+                        pend_f = f < pend_f ? f : pend_f;
+                } else {
+                    generated++;
+                    if (f >= bound)
+                        valid = false;
+                }
             }
             if (valid) {
                 if constexpr (kOneRound) {
@@ -1562,6 +1635,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             route_child<KW, kPfSlots, SH>(a, P, st, f0, w, valid, owner == P.shard, owner, ck, g, h, m, claimed, ovf, lp,
                                       false, has_pf && r == 0, pf);
             BPHASE(9)
+        }
+        if constexpr (kPartial) {
+            if (partial_k >= 0) {  // uniform
+                // the parent again, under the lowest f it has left
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_xor(pend_f, o);
+                    if (o < lpn)
+                        pend_f = y < pend_f ? y : pend_f;
+                }
+                // (queued `partial_ahead` buckets before its first child is
+                // due, but past this batch: the children are then in their
+                // buckets before those are cut, not after; the entry keeps
+                // the f the parent resumes from)
+                const bool again = ok && glane == 0 && pend_f != kIntMax;
+                part_q += again;
+                const Entry pe = {local ? le.slot : e.slot, pend_f | kPartialBit};
+                int pb = bucket_of(pend_f, f0, w) - partial_ahead;
+                pb = pb < view.batch_b + view.batch_nb ? view.batch_b + view.batch_nb : pb;
+                open_append(a, lp, again, pb, pe, st, false);
+            }
         }
         BPHASE(7)
     };
@@ -1587,7 +1681,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     const int passes = masks > 64 ? masks / 64 : 1;
     const unsigned long long rounds = (unsigned long long)ctl->deep_blocks / (nact * passes);
     const int depth = rounds >= (unsigned long long)ctl->deep_rounds ? view.depth : 1;
-    const int f_limit = f0 + (int)(((long long)view.batch_b + view.batch_nb) << w);
     __shared__ LEntry<KW> lq[2][kLocalCap];
     __shared__ int lq_count[2], out_n;
     __shared__ Entry outq[kOutCap];
@@ -1840,7 +1933,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             for (int k = 0; k < kPer; k++) {
                 const int i = k * kBlock + threadIdx.x;
                 e[k] = i < no ? outq[i] : Entry{0, 0};
-                bk[k] = i < no ? bucket_of(e[k].f, f0, w) : kBuckets;
+                bk[k] = i < no ? bucket_of(entry_f(e[k]), f0, w) : kBuckets;
+                if (kPartial && i < no && e[k].f < 0) {  // a parent with children left: queued ahead of them
+                    const int pb = bk[k] - partial_ahead, be = view.batch_b + view.batch_nb;
+                    bk[k] = pb < be ? be : pb;
+                }
                 if (i < no)
                     atomicMin(&fb_min, bk[k]);
             }
@@ -1875,6 +1972,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);
     stale = wave_sum(stale);
+    if constexpr (kPartial) {
+        part_q = wave_sum(part_q);
+        part_t = wave_sum(part_t);
+    }
     if (lane == 0) {
         unsigned long long *row = stat_row(st, blockIdx.x * kWaves + wave);
         if (expanded)
@@ -1889,6 +1990,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             atomicAdd(&row[kStOvfTable], (unsigned long long)ovf);
         if (stale)
             atomicAdd(&row[kStDropped], (unsigned long long)stale);
+        if constexpr (kPartial) {
+            if (part_q)
+                atomicAdd(&row[kStPartQueued], (unsigned long long)part_q);
+            if (part_t)
+                atomicAdd(&row[kStPartTaken], (unsigned long long)part_t);
+        }
     }
 #ifdef PASTAR_PHASE_TIMERS
     if ((view.timing & 4) && timing && threadIdx.x == 0) {

@@ -1089,6 +1089,7 @@ struct SearchCfg {
     int xlag;                        // steps the select may run ahead of the insert of received records (0, 1)
     int table_log2;
     int verbose, profile, eager, depth;
+    int partial_k;  // partial expansion window in buckets (negative: off)
     int64_t max_steps;
     int64_t band;
 };
@@ -1361,6 +1362,20 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         hc.deep_rounds = e && *e ? std::max(1, std::atoi(e)) : (c->n <= 6 ? 1 : (1 << 30));
     }
     hc.batch_nb = 1;
+    hc.prune_f = kIntMax;
+    if (const char *e = std::getenv("PASTAR_PRUNE_F"))  // diagnostics: a known upper bound of the optimum
+        hc.prune_f = std::atoi(e) + 1;                  // (what a bound of that quality would be worth)
+    // partial expansion (N >= 7; tools/gpu/partial_probe.py): a window of one
+    // bucket past the batch, the parent queued in the bucket of its first
+    // waiting child, every child it has left generated when it comes up again
+    hc.partial_k = cfg.partial_k;
+    if (const char *e = std::getenv("PASTAR_PARTIAL_K"))  // tuning overrides
+        hc.partial_k = std::atoi(e);
+    if (const char *e = std::getenv("PASTAR_PARTIAL_AHEAD"))
+        hc.partial_ahead = std::max(0, std::atoi(e));
+    hc.partial_two = 1;
+    if (const char *e = std::getenv("PASTAR_PARTIAL_TWO"))
+        hc.partial_two = std::atoi(e);
     hc.spin_limit = c->spin_limit;
     hc.low_b = kBuckets;
     // (kinase at 8 shards: 147 steps at 4 buckets, 124 at 8; syn8x400: 10.9 M
@@ -1883,6 +1898,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     res->expand_ms = expand_ms;
     res->select_ms = (double)h.select_ticks * 1e-5;
+    if (cfg.verbose && h.partial_k >= 0)
+        std::fprintf(stderr, "[pastar] partial expansion (window %d buckets): %llu parents queued again, %llu taken again, "
+                     "%llu entries dropped\n", h.partial_k, h.part_queued, h.part_taken, h.dropped);
     if (cfg.verbose && cfg.profile) {
         std::fprintf(stderr, "[pastar] select phases (us/launch):");
         for (int k = 0; k < 4; k++)
@@ -2210,6 +2228,9 @@ int pastar_gpu_search(pastar_ctx *c, const pastar_search_opts *opts, pastar_resu
     if (cfg.xblock_recs > (1ull << 24))
         return fail(PASTAR_EINVAL, "xchg_block_records %llu above 2^24", cfg.xblock_recs);
     cfg.xlag = o.xchg_lag;
+    if (o.partial < -1 || o.partial > 1024)
+        return fail(PASTAR_EINVAL, "partial %d outside [-1, 1024]", o.partial);
+    cfg.partial_k = o.partial == 0 ? 1 : o.partial - 1;  // (-1: off)
     if (const char *e = std::getenv("PASTAR_XCHG_LAG"))  // tuning override
         cfg.xlag = std::atoi(e);
     if (cfg.xlag < 0 || cfg.xlag > 1)
@@ -2674,6 +2695,7 @@ int pastar_gpu_lists_reset(pastar_ctx *c, const pastar_search_opts *opts)
     PA_TRY(ensure_hc(c));
     PA_TRY(ensure_origin(c));
     SearchCfg cfg{};
+    cfg.partial_k = -1;
     cfg.kmax = cfg.kmin = 1;
     cfg.table_log2 = o.table_slots_log2 > 0 ? (int)o.table_slots_log2 : 20;
     if (cfg.table_log2 < 10 || cfg.table_log2 > 32)
@@ -2982,6 +3004,7 @@ int pastar_gpu_search_many(pastar_ctx *const *ctxs, int count, const pastar_sear
     if (opts)
         o = *opts;
     SearchCfg cfg{};
+    cfg.partial_k = -1;
     cfg.verbose = o.verbose;
     cfg.band = o.band;
     cfg.max_steps = o.max_steps;

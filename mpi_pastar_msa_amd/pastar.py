@@ -131,6 +131,7 @@ class PAStarOpt:
     mode: str = "auto"  # "auto": LDS-resident search when the problem fits; "batched"; "solo"
     xchg_lag: int = 0   # sharded: 1 = the exchange of step i runs beside the expansion of step i + 1
     xchg_block_records: int = 0  # sharded: records one step carries to one shard (0 = default)
+    partial: int = 0    # partial expansion for N >= 7: 0 = default (window of one bucket), n > 0: n - 1 buckets, -1: off
 
     def search_opts(self):
         return nat.pastar_search_opts(self.batch_nodes, self.batch_min, self.table_slots_log2, self.pool_entries,
@@ -138,7 +139,7 @@ class PAStarOpt:
                                       int(self.verbose),
                                       int(not self.autogrow), int(self.eager), int(self.depth),
                                       {"auto": 0, "batched": 1, "solo": 2}[self.mode],
-                                      int(self.xchg_lag), 0, int(self.xchg_block_records))
+                                      int(self.xchg_lag), int(self.partial), int(self.xchg_block_records))
 
 
 def compute_weights(seqs):

@@ -140,6 +140,48 @@ def test_search_n8(name, kat):
         assert o.alignment_cost(rows) == ref["score"]
 
 
+@pytest.mark.parametrize("partial", [1, 2, 4])
+def test_partial_expansion_same_alignment(partial, kat):
+    """Partial expansion (N >= 7: children past a window beyond the step's
+    buckets wait until their parent comes up again): every window gives the
+    score and the alignment of the search that generates every child at
+    once, and generates fewer children."""
+    ref = kat["inputs"]["syn8x100_s3"]
+    seqs = Sequences.from_fasta(golden(ref["file"]))
+    o = orc.Oracle(fasta=golden(ref["file"]))
+    with Engine(seqs).init() as e:
+        full = e.pa_star(PAStarOpt(partial=-1))
+        rows_full = e.alignment()
+    with Engine(seqs).init() as e:
+        part = e.pa_star(PAStarOpt(partial=partial))
+        rows = e.alignment()
+        goal = e.closed_lookup(e.sequences.get_final_coord())
+    assert full.score == part.score == ref["score"]
+    assert rows == rows_full
+    assert o.alignment_cost(rows) == ref["score"]
+    assert goal is not None and goal.g == ref["score"]
+    assert part.generated < full.generated and part.table_used < full.table_used
+
+
+def test_partial_expansion_random_problems_match_oracle():
+    """7 and 8 short sequences, tiny batches (many steps, parents taken again
+    in later steps), each partial-expansion window against the oracle."""
+    rng = random.Random(23)
+    alphabet = "ACDEFGHIKLMNPQRSTVWY"
+    for trial in range(6):
+        n = 7 + trial % 2
+        seqs = ["".join(rng.choice(alphabet[:4 + trial]) for _ in range(rng.randint(1, 6))) for _ in range(n)]
+        o = orc.Oracle(seqs=seqs)
+        ref = o.astar()
+        for partial in (-1, 1, 2, 3):
+            with Engine(seqs).init() as e:
+                r = e.pa_star(PAStarOpt(mode="batched", partial=partial, batch_nodes=rng.choice([1, 8, 0])))
+                assert r.score == ref["score"], (seqs, partial, r, ref)
+                rows = e.alignment()
+                assert o.alignment_cost(rows) == ref["score"]
+                assert [row.replace("-", "") for row in rows] == seqs
+
+
 @pytest.mark.parametrize("mode", ["batched", "auto"])
 def test_random_small_problems_match_oracle(mode):
     rng = random.Random(7)
