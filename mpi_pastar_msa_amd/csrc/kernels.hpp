@@ -493,7 +493,7 @@ struct Ctl {
     alignas(128) unsigned long long k_start, k_end, expand_ticks, timed_launches;
     unsigned long long select_ticks, gap_ticks, prev_end;
     unsigned long long phase_ticks[8];  // profile: select phases (diagnostics)
-    unsigned long long body_ticks[12];  // profile: expand phases of block 0 (diagnostics)
+    unsigned long long body_ticks[18];  // profile: expand phases of block 0 (diagnostics; 10, 11: dive counts; 12..: dive phases)
     unsigned long long body_launches;
     // profile (PASTAR_PHASE_TIMERS builds): per-block chain statistics,
     // {blocks, sum levels, max levels, sum rounds, max rounds, max ticks},
@@ -814,6 +814,47 @@ __device__ __forceinline__ void open_append(const SearchArgs &a, const LocalPush
     queue_append(a, pred, b, e, st, may_lower);
 }
 
+// Queue an improved child of this shard: into the block-local continuation
+// queue when its f lies in the batch's buckets and the queue has room, else
+// into the open list.  Every lane of the wave must call it.
+template <int KW>
+__device__ __forceinline__ void queue_improved(const SearchArgs &a, StepStats *st, int f0, int w, bool pred,
+                                               int64_t slot, const uint64_t (&ck)[KW], int g, int h, int m,
+                                               const LocalPush<KW> &lp, bool may_lower = false)
+{
+    const int f = g + h;
+    const Entry e = {(uint32_t)slot, f};
+    bool global = pred;
+    if (lp.buf) {
+        const bool want = pred && f < lp.f_limit;
+        const uint64_t mask = __ballot(want);
+        if (mask) {
+            const int lane = lane_id();
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader)
+                base = atomicAdd(lp.count, __popcll(mask));
+            base = bcast_lane(base, leader);
+            if (want) {
+                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (pos < lp.cap) {
+                    LEntry<KW> le;
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        le.key[k] = ck[k];
+                    le.slot = (uint32_t)slot;
+                    le.g = g;
+                    le.h = h;
+                    le.pmask = m;
+                    lp.buf[pos] = le;
+                    global = false;
+                }
+            }
+        }
+    }
+    open_append(a, lp, global, bucket_of(f, f0, w), e, st, may_lower);
+}
+
 // Route one child: relax locally or post it to its owner shard; queue the
 // improved ones (block-local continuation queue first, when it qualifies).
 // All lanes of the wave must call it.
@@ -858,37 +899,7 @@ __device__ __forceinline__ void route_child(const SearchArgs &a, const PP &P, St
                 atomicMin(a.goal_g, g);
         }
     }
-    const int f = g + h;
-    const Entry e = {(uint32_t)slot, f};
-    bool global = improved && local;
-    if (lp.buf) {
-        const bool want = improved && local && f < lp.f_limit;
-        const uint64_t mask = __ballot(want);
-        if (mask) {
-            const int lane = lane_id();
-            const int leader = __ffsll((long long)mask) - 1;
-            int base = 0;
-            if (lane == leader)
-                base = atomicAdd(lp.count, __popcll(mask));
-            base = bcast_lane(base, leader);
-            if (want) {
-                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-                if (pos < lp.cap) {
-                    LEntry<KW> le;
-#pragma unroll
-                    for (int k = 0; k < KW; k++)
-                        le.key[k] = ck[k];
-                    le.slot = (uint32_t)slot;
-                    le.g = g;
-                    le.h = h;
-                    le.pmask = m;
-                    lp.buf[pos] = le;
-                    global = false;
-                }
-            }
-        }
-    }
-    open_append(a, lp, global, bucket_of(f, f0, w), e, st, remote_in);
+    queue_improved<KW>(a, st, f0, w, improved && local, slot, ck, g, h, m, lp, remote_in);
     if (SH && P.n_shards > 1) {
         const bool remote = valid && !local && lowered;
         Remote<KW> rec;
@@ -1328,6 +1339,43 @@ __device__ __forceinline__ Entry batch_entry_at(const SearchArgs &a, const SelVi
 }
 
 
+// ---------------------------------------------------------------------------
+// The dive (N = 4, 1-word keys): several continuation levels per memory round
+// trip.  A block-local chain is bound by latency: a level costs two dependent
+// memory round trips (the parent's pair cells, then the children's claim or
+// atomicMin) and a pass over one wave's worth of instructions.  When a level's
+// few parents sit close together, every node within kDiveW steps of them lies
+// in one small window of the lattice: the window's pair cells ((kDiveW + 1)^2
+// per pair) come in ONE gather, the next kDiveW levels are then expanded out of
+// LDS alone -- a child continues when it improves on what the dive itself has
+// seen of its node (a direct-mapped table over the window's relative
+// coordinates) and its f stays in the batch's buckets -- and every child
+// generated on the way is relaxed into the node table afterwards, all at
+// once.  Only then is a continued node known to have been an improvement
+// (its own relax says so): one that was not has been expanded for nothing,
+// which costs work but never a wrong g (every g written is the cost of a
+// real path).
+// ---------------------------------------------------------------------------
+#ifndef PASTAR_DIVE
+#define PASTAR_DIVE 1
+#endif
+constexpr int kDiveW = 6;               // levels per dive; nodes up to kDiveW steps past the window's origin
+static_assert(kDiveW <= 8, "4-bit window coordinates");
+constexpr int kDiveWS = kDiveW + 1;
+constexpr int kDiveCells = kDiveWS * kDiveWS;
+constexpr int kDiveNodes = kDiveWS * kDiveWS * kDiveWS * kDiveWS;
+#ifndef PASTAR_DIVE_SPREAD
+#define PASTAR_DIVE_SPREAD (kDiveW - 2)
+#endif
+constexpr int kDiveMaxSpread = PASTAR_DIVE_SPREAD;  // start nodes at most this far apart
+constexpr int kDiveFront = 4;           // nodes one dive level expands (the lane groups of one wave)
+constexpr int kDiveRecs = 384;          // children one dive generates at most
+struct DiveRec {
+    uint64_t key;
+    int g, h, info;  // info: parent mask | kDiveCont
+};
+constexpr int kDiveCont = 0x100;        // expanded inside the dive
+
 // expand every entry of the batch (worker_inner's dequeue, closed check and
 // getNeigh, PAStar.cpp:320-401) and relax its neighbours into the node table
 // (PAStar::enqueue + conditional_enqueue, :219-237).
@@ -1389,6 +1437,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
     // parent's 15 children and their 15 x 15 children on the block's 16
     // groups); the key increment of this group's child mask
     constexpr bool kTwoLevel = N == 4 && KW == 1;
+    constexpr bool kDive = PASTAR_DIVE && N == 4 && KW == 1;  // (the two-level pass when built without)
     uint64_t kinc_grp[KW];
     {
         const uint64_t zero[KW] = {};
@@ -1768,7 +1817,318 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if (threadIdx.x == 0)
             lq_count[nxt] = 0;
         lds_barrier();
-        if constexpr (kTwoLevel) {
+        if constexpr (kDive) {
+            // the level's nodes (at most kDiveFront), the window's origin (their
+            // componentwise lowest position) and their spread: every wave
+            // computes them for itself (no barrier).  Every start node needs a
+            // level ahead of it in the window; a level whose nodes lie
+            // further apart takes the one-level pass below.
+            bool dive = cnt <= kDiveFront && lvl + kDiveW < depth && (!SH || P.n_shards == 1);
+            int org[N];
+            LEntry<KW> mine{};
+            int mpos[N];
+            constexpr bool elig = true;
+            if (dive) {  // uniform
+                const int li = lane & (kDiveFront - 1);
+                mine = lq[cur][li < cnt ? li : 0];
+                const uint64_t mk[KW] = {mine.key[0]};
+                decode_key<N, KW>(P, n, mk, mpos);
+                int spread = 0;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    int lo = mpos[i], hi = mpos[i];
+                    if (cnt > 1) {  // uniform
+#pragma unroll
+                        for (int o = 1; o < kDiveFront; o <<= 1) {
+                            const int yl = __shfl_xor(lo, o), yh = __shfl_xor(hi, o);
+                            lo = yl < lo ? yl : lo;
+                            hi = yh > hi ? yh : hi;
+                        }
+                    }
+                    org[i] = __builtin_amdgcn_readfirstlane(lo);
+                    const int sp = __builtin_amdgcn_readfirstlane(hi) - org[i];
+                    spread = sp > spread ? sp : spread;
+                }
+                dive = spread <= kDiveMaxSpread;
+            }
+            if (dive) {
+                constexpr int NP = N * (N - 1) / 2;
+                __shared__ int2 cw[NP][kDiveCells];
+                __shared__ int relbest[kDiveNodes];
+                __shared__ DiveRec recs[kDiveRecs];
+                __shared__ int rec_n, dive_done;
+                auto rel_index = [](int rel) {
+                    return (((rel & 15) * kDiveWS + ((rel >> 4) & 15)) * kDiveWS + ((rel >> 8) & 15)) * kDiveWS +
+                           ((rel >> 12) & 15);
+                };
+                // ---- the window's pair cells (one gather), the start nodes' slot words
+                constexpr int kCT = (NP * kDiveCells + kBlock - 1) / kBlock;
+                int2 cell[kCT];
+#pragma unroll
+                for (int t = 0; t < kCT; t++) {
+                    const int ct = threadIdx.x + t * kBlock;
+                    cell[t] = make_int2(0, 0);
+                    if (ct < NP * kDiveCells) {
+                        const int p = ct / kDiveCells, r = ct % kDiveCells, i = r / kDiveWS, j = r % kDiveWS;
+                        const PairConst k = pc[p];
+                        int ox = 0, oy = 0;
+#pragma unroll
+                        for (int d = 0; d < N; d++) {
+                            if (d == k.x)
+                                ox = org[d];
+                            if (d == k.y)
+                                oy = org[d];
+                        }
+                        const int ix = ox + i, iy = oy + j;
+                        if (ix <= k.lx && iy <= k.ly) {
+                            const __attribute__((address_space(1))) int2 *cells =
+                                (const __attribute__((address_space(1))) int2 *)(P.HC + k.off);
+                            const int64_t at = (int64_t)ix * k.row + iy;
+                            cell[t] = make_int2(cells[at].x, cells[at].y);
+                        }
+                    }
+                }
+                uint64_t sbest = 0, saux = 0;
+                const bool starter = wave == 0 && lane < cnt;
+                if (starter) {
+                    const uint64_t *ps = a.table + (uint64_t)mine.slot * SW;
+                    sbest = ps[KW];
+                    saux = ps[KW + 1];
+                }
+                for (int k = threadIdx.x; k < kDiveNodes; k += kBlock)
+                    relbest[k] = kIntMax;
+#pragma unroll
+                for (int t = 0; t < kCT; t++) {
+                    const int ct = threadIdx.x + t * kBlock;
+                    if (ct < NP * kDiveCells)
+                        cw[ct / kDiveCells][ct % kDiveCells] = cell[t];
+                }
+                lds_barrier();
+                BPHASE(12)
+                // ---- wave 0 alone runs the levels, out of LDS and registers
+                // (no block barrier inside): each of its lane groups holds
+                // one node of the level, lane m of the group its child m
+                if (wave == 0) {
+                    const LocalPush<KW> lq_back{lq[nxt], &lq_count[nxt], f_limit, lq_cap, outq, &out_n};
+                    bool okp = false;
+                    int nrel = 0;
+                    if (starter) {
+                        // a start node, as a one-level continuation entry
+                        const bool okb = mine.g + mine.h < bound;
+                        okp = okb && (uint32_t)(sbest >> 32) >= (uint32_t)mine.g;
+                        stale += okb && !okp;
+                        if (okp && elig) {
+                            reopen += (int)(uint32_t)saux != kIntMax;
+                            *(int *)(a.table + (uint64_t)mine.slot * SW + KW + 1) = mine.g;
+                            expanded++;
+#pragma unroll
+                            for (int i = 0; i < N; i++)
+                                nrel |= (mpos[i] - org[i]) << (4 * i);
+                            atomicMin(&relbest[rel_index(nrel)], mine.g);
+                        }
+                    }
+                    // (a current node outside the window: back into the queue as it is)
+                    {
+                        const uint64_t bk[KW] = {mine.key[0]};
+                        queue_improved<KW>(a, st, f0, w, starter && okp && !elig, mine.slot, bk, mine.g, mine.h, mine.pmask,
+                                           lq_back);
+                    }
+                    okp = okp && elig;
+                    // this lane's child: its mask's constants
+                    const int m = glane;
+                    const int relinc = (m & 1) | ((m >> 1) & 1) << 4 | ((m >> 2) & 1) << 8 | ((m >> 3) & 1) << 12;
+                    const int idxinc = rel_index(relinc);
+                    // equal gap costs (the reference's): the gap part of the child's cost depends on the mask alone
+                    const bool eqgap = P.gap_open == P.gap_ext;
+                    int coff[NP], gapw[NP], dg_const = 0, both = 0;
+                    {
+                        int p = 0;
+#pragma unroll
+                        for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+                            for (int y = x + 1; y < N; y++, p++) {
+                                const int bx = (m >> x) & 1, by = (m >> y) & 1;
+                                coff[p] = bx * kDiveWS + by;
+                                gapw[p] = pc[p].w;
+                                if (bx & by)
+                                    both |= 1 << p;
+                                else
+                                    dg_const += ((bx | by) ? P.gap_open : P.gap_gap) * gapw[p];
+                            }
+                        }
+                    }
+                    // near the lattice's far border a coordinate may be at its end
+                    bool edge = false;
+#pragma unroll
+                    for (int i = 0; i < N; i++)
+                        edge |= org[i] + kDiveW >= P.len[i];
+                    // the level's nodes: the first kDiveFront set lanes of `pick`, one per lane group
+                    uint64_t nkey = mine.key[0], ckey = 0;
+                    int ng = mine.g, npm = mine.pmask, nidx = rel_index(nrel);
+                    bool nact = false;
+                    uint64_t pick = __ballot(okp);
+                    auto hand_over = [&](uint64_t key_v, int g_v, int pm_v, int rel_v, int idx_v, bool pm_is_lane) {
+                        uint64_t k_o = 0;
+                        int g_o = 0, pm_o = 0, rel_o = 0, idx_o = 0;
+                        bool act_o = false;
+#pragma unroll
+                        for (int q = 0; q < kDiveFront; q++) {
+                            const bool any = pick != 0;  // uniform
+                            const int src = any ? __ffsll((long long)pick) - 1 : 0;
+                            pick &= pick - 1;
+                            const uint64_t kq = bcast_lane((unsigned long long)key_v, src);
+                            const int gq = bcast_lane(g_v, src), relq = bcast_lane(rel_v, src), idxq = bcast_lane(idx_v, src);
+                            const int pmq = pm_is_lane ? (src & (lpn - 1)) : bcast_lane(pm_v, src);
+                            if (group == q) {
+                                k_o = kq;
+                                g_o = gq;
+                                pm_o = pmq;
+                                rel_o = relq;
+                                idx_o = idxq;
+                                act_o = any;
+                            }
+                        }
+                        nkey = k_o;
+                        ng = g_o;
+                        npm = pm_o;
+                        nrel = rel_o;
+                        nidx = idx_o;
+                        nact = act_o;
+                    };
+                    hand_over(nkey, ng, npm, nrel, nidx, false);
+                    int rec_cnt = 0, done = 0;
+                    for (int d = 0; d < kDiveW; d++) {
+                        if (!__ballot(nact) || rec_cnt + kDiveFront * (masks - 1) > kDiveRecs)
+                            break;  // uniform
+                        done++;
+                        int blocked = 0, dg = 0, hh = 0;
+                        if (edge) {  // uniform
+#pragma unroll
+                            for (int i = 0; i < N; i++)
+                                blocked |= (org[i] + ((nrel >> (4 * i)) & 15) >= P.len[i]) << i;
+                        }
+                        if (eqgap) {  // uniform
+                            dg = dg_const;
+                            int p = 0;
+#pragma unroll
+                            for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+                                for (int y = x + 1; y < N; y++, p++) {
+                                    const int base = ((nrel >> (4 * x)) & 15) * kDiveWS + ((nrel >> (4 * y)) & 15);
+                                    const int2 ch = cw[p][base + coff[p]];
+                                    const int2 c0 = cw[p][base];
+                                    hh += ch.x;
+                                    dg += ((both >> p) & 1) ? c0.y : 0;
+                                }
+                            }
+                        } else {
+                            int p = 0;
+#pragma unroll
+                            for (int x = 0; x < N - 1; x++) {
+#pragma unroll
+                                for (int y = x + 1; y < N; y++, p++) {
+                                    const int bx = (m >> x) & 1, by = (m >> y) & 1;
+                                    const int base = ((nrel >> (4 * x)) & 15) * kDiveWS + ((nrel >> (4 * y)) & 15);
+                                    const int2 ch = cw[p][base + coff[p]];
+                                    const int2 c0 = cw[p][base];
+                                    hh += ch.x;
+                                    // one moves, the other idles: gap open iff the idle one moved into the node
+                                    const int idle = bx ? y : x;
+                                    const int g0 =
+                                        (bx | by) ? (((npm >> idle) & 1) ? P.gap_open : P.gap_ext) : P.gap_gap;
+                                    dg += (bx & by) ? c0.y : g0 * gapw[p];
+                                }
+                            }
+                        }
+                        const int g = ng + dg, f = g + hh;
+                        const bool valid = nact && m >= 1 && !(m & blocked);
+                        generated += valid;
+                        const bool keep = valid && f < bound;
+                        const int relc = nrel + relinc, cidx = nidx + idxinc;
+                        // (a coordinate at kDiveW has no cells ahead of it in the window: not expanded
+                        // here; coordinates are at most kDiveW <= 8, so adding 8 - kDiveW sets a
+                        // field's top bit exactly there)
+                        const bool inside = ((relc + (8 - kDiveW) * 0x1111) & 0x8888) == 0;
+                        bool cont = false;
+                        if (keep) {
+                            const int old = atomicMin(&relbest[cidx], g);
+                            cont = old > g && f < f_limit && inside && d + 1 < kDiveW;
+                        }
+                        const uint64_t km = __ballot(keep);
+                        const int ri = rec_cnt + __popcll(km & ((1ull << lane) - 1ull));
+                        rec_cnt += __popcll(km);
+                        // the first kDiveFront continuing children are the next level
+                        pick = __ballot(cont);
+                        {
+                            uint64_t rest = pick;
+#pragma unroll
+                            for (int q = 0; q < kDiveFront; q++)
+                                rest &= rest - 1;
+                            cont = cont && !((rest >> lane) & 1ull);
+                        }
+                        ckey = nkey + kinc[0];
+                        if (keep)
+                            recs[ri] = DiveRec{ckey, g, hh, m | (cont ? kDiveCont : 0)};
+                        hand_over(ckey, g, 0, relc, cidx, true);
+                    }
+                    if (lane == 0) {
+                        rec_n = rec_cnt;
+                        dive_done = done;
+                    }
+                }
+                lds_barrier();
+                BPHASE(13)
+                // ---- every generated child into the node table, at once, by the whole block
+                const int nrec = rec_n, done = dive_done;
+                const LocalPush<KW> lq_dive{lvl + done < depth ? lq[nxt] : nullptr, &lq_count[nxt], f_limit, lq_cap,
+                                            outq, &out_n};
+                for (int base = 0; base < nrec; base += kBlock) {
+                    const int r = base + threadIdx.x;
+                    const bool has = r < nrec;
+                    const DiveRec rc = recs[has ? r : 0];
+                    const uint64_t ck[KW] = {rc.key};
+                    bool imp = false, cl = false;
+                    int64_t slot = 0;
+                    if (has) {
+                        slot = relax<KW, kPfSlots>(a.table, a.cap_mask, ck, rc.g, rc.info & 15, rc.h, imp, cl, false,
+                                                   SlotWords<KW, kPfSlots>{});
+                        if (slot < 0) {
+                            ovf++;
+                            imp = false;
+                            slot = 0;
+                        }
+                        claimed += cl;
+                        if (imp && rc.key == P.goal_key[0])
+                            atomicMin(a.goal_g, rc.g);
+                    }
+                    const bool was_cont = has && (rc.info & kDiveCont);
+                    if (was_cont && imp) {
+                        // an expansion that counted: close the node (a min: the old value tells a reopening)
+                        const int old = atomicMin((int *)(a.table + (uint64_t)slot * SW + KW + 1), rc.g);
+                        reopen += old != kIntMax;
+                        expanded++;
+                    }
+                    queue_improved<KW>(a, st, f0, w, has && imp && !was_cont, slot, ck, rc.g, rc.h, rc.info & 15, lq_dive);
+                }
+                BLK_COUNT(done, 1)
+                BPHASE(14)
+#ifdef PASTAR_PHASE_TIMERS
+                if ((view.timing & 4) && timing && threadIdx.x == 0) {
+                    atomicAdd(&ctl->body_ticks[10], 1ull);                       // dives
+                    atomicAdd(&ctl->body_ticks[11], (unsigned long long)done);   // their levels
+                    atomicAdd(&ctl->phase_ticks[4 + (done < 3 ? done : 3)], 1ull);  // dives of 0, 1, 2, 3+ levels
+                    atomicAdd(&ctl->phase_ticks[cnt == 1 ? 0 : 1], 1ull);        // one start node / several
+                    atomicAdd(&ctl->phase_ticks[2], (unsigned long long)nrec);   // children generated
+                }
+#endif
+                lds_barrier();
+                BPHASE(3)
+                cur = nxt;
+                lvl += done > 0 ? done - 1 : 0;
+                continue;
+            }
+        }
+        if constexpr (kTwoLevel && !kDive) {
             if (cnt == 1 && lvl + 1 < depth && (!SH || P.n_shards == 1)) {
                 // one parent: this level and the next in one pass.  The next
                 // level of the one-level pass would expand exactly this

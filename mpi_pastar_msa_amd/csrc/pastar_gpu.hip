@@ -1898,7 +1898,7 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
     }
     res->expand_ms = expand_ms;
     res->select_ms = (double)h.select_ticks * 1e-5;
-    if (cfg.verbose && h.partial_k >= 0)
+    if (cfg.verbose && h.partial_k >= 0 && (c->n >= 7 || h.part_queued))
         std::fprintf(stderr, "[pastar] partial expansion (window %d buckets): %llu parents queued again, %llu taken again, "
                      "%llu entries dropped\n", h.partial_k, h.part_queued, h.part_taken, h.dropped);
     if (cfg.verbose && cfg.profile) {
@@ -1914,6 +1914,13 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                      h.blk_stats[3] / nb, h.blk_stats[4], h.blk_stats[5] * 1e-2);
         std::fprintf(stderr, "[pastar] continuation levels by parents: 1: %llu, 2-4: %llu, 5-16: %llu, more: %llu\n",
                      h.blk_stats[6], h.blk_stats[7], h.blk_stats[8], h.blk_stats[9]);
+        std::fprintf(stderr, "[pastar] dive phases of block 0 (us/launch): gather %.2f levels %.2f relax %.2f\n",
+                     (double)h.body_ticks[12] * 1e-2 / std::max<double>(1.0, (double)h.body_launches),
+                     (double)h.body_ticks[13] * 1e-2 / std::max<double>(1.0, (double)h.body_launches),
+                     (double)h.body_ticks[14] * 1e-2 / std::max<double>(1.0, (double)h.body_launches));
+        std::fprintf(stderr, "[pastar] dives %llu (one start node %llu, several %llu), levels %llu, by levels 0: %llu 1: %llu "
+                     "2: %llu 3+: %llu, children %llu\n", h.body_ticks[10], h.phase_ticks[0], h.phase_ticks[1], h.body_ticks[11],
+                     h.phase_ticks[4], h.phase_ticks[5], h.phase_ticks[6], h.phase_ticks[7], h.phase_ticks[2]);
     }
     res->gap_ms = (double)h.gap_ticks * 1e-5;
     res->expand_launches = launches;
