@@ -768,6 +768,14 @@ struct LocalPush {
     int cap;     // entries one level may take (a block's width per round)
     Entry *out;  // block's outgoing buffer for the open list, appended once
     int *out_n;  // at the end of the launch (nullptr: append at once)
+    // A kernel that runs beside a select (the sharded search's insert with
+    // xchg_lag = 1) must not append to the open list itself: a select could
+    // cut a position that is reserved but not yet written.  Its entries go to
+    // a staging array instead, which a launch on the select's own stream
+    // appends later (xdrain_kernel).
+    Entry *stage;
+    unsigned long long *stage_n;
+    unsigned long long stage_cap;
 };
 
 constexpr int kOutCap = 1024;  // entries a block defers to its final append
@@ -793,6 +801,10 @@ template <int KW>
 __device__ __forceinline__ void open_append(const SearchArgs &a, const LocalPush<KW> &lp, bool pred, int b,
                                             const Entry &e, StepStats *st, bool may_lower)
 {
+    if (lp.stage) {
+        wave_append(pred, lp.stage_n, lp.stage, lp.stage_cap, e, &st->ovf_near);
+        return;
+    }
     if (lp.out) {
         const uint64_t mask = __ballot(pred);
         if (mask) {
@@ -1359,7 +1371,10 @@ __device__ __forceinline__ Entry batch_entry_at(const SearchArgs &a, const SelVi
 #ifndef PASTAR_DIVE
 #define PASTAR_DIVE 1
 #endif
-constexpr int kDiveW = 6;               // levels per dive; nodes up to kDiveW steps past the window's origin
+#ifndef PASTAR_DIVE_W
+#define PASTAR_DIVE_W 6
+#endif
+constexpr int kDiveW = PASTAR_DIVE_W;               // levels per dive; nodes up to kDiveW steps past the window's origin
 static_assert(kDiveW <= 8, "4-bit window coordinates");
 constexpr int kDiveWS = kDiveW + 1;
 constexpr int kDiveCells = kDiveWS * kDiveWS;
@@ -2103,9 +2118,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                     }
                     const bool was_cont = has && (rc.info & kDiveCont);
                     if (was_cont && imp) {
-                        // an expansion that counted: close the node (a min: the old value tells a reopening)
-                        const int old = atomicMin((int *)(a.table + (uint64_t)slot * SW + KW + 1), rc.g);
-                        reopen += old != kIntMax;
+                        // an expansion that counted: close the node.  A slot claimed just now was
+                        // never closed (a plain store); else a min, whose old value tells a reopening
+                        int *closed = (int *)(a.table + (uint64_t)slot * SW + KW + 1);
+                        if (cl) {
+                            *closed = rc.g;
+                        } else {
+                            const int old = atomicMin(closed, rc.g);
+                            reopen += old != kIntMax;
+                        }
                         expanded++;
                     }
                     queue_improved<KW>(a, st, f0, w, has && imp && !was_cont, slot, ck, rc.g, rc.h, rc.info & 15, lq_dive);
@@ -2491,6 +2512,40 @@ __global__ __launch_bounds__(kBlock) void insert_remote_kernel(SearchArgs a, con
     }
 }
 
+// The staged open-list entries of an insert that ran beside a select
+// (xchg_lag = 1), appended on the select's own stream: every entry is written
+// before the next select can cut it.  The count is cleared by the launch's
+// last block for the insert that uses the staging array next.
+__global__ __launch_bounds__(kBlock) void xdrain_kernel(SearchArgs a, const Entry *__restrict__ stage,
+                                                        unsigned long long *stage_n, unsigned long long stage_cap,
+                                                        unsigned *arrive)
+{
+    const Ctl *ctl = a.ctl;
+    if (ld_agent(&ctl->status))
+        return;
+    const int w = ctl->band_log2, f0 = ctl->f0;
+    unsigned long long n = ld_agent(stage_n);
+    n = n < stage_cap ? n : stage_cap;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    const unsigned long long iters = (n + stride - 1) / stride;
+    for (unsigned long long it = 0; it < iters; it++) {
+        const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x + it * stride;
+        const bool has = i < n;
+        const Entry e = has ? stage[i] : Entry{0, 0};
+        queue_append(a, has, bucket_of(e.f, f0, w), e, a.stats, true);
+    }
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        st_agent(stage_n, 0ull);
+        st_agent(arrive, 0u);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Shard exchange kernels (side stream).  One step:
 //   xpack    ring -> fixed-size blocks, one per destination shard, each with
@@ -2514,6 +2569,10 @@ struct XArgs {
     unsigned char *recv;  // [n_shards] blocks of block_bytes
     unsigned long long block_bytes, block_recs;
     int n_shards, shard, step, lag;
+    // lag 1: the open-list entries of this step's received records (see LocalPush::stage)
+    Entry *stage;
+    unsigned long long *stage_n;
+    unsigned long long stage_cap;
 };
 
 __device__ __forceinline__ XHdr *xblock_hdr(unsigned char *blocks, unsigned long long block_bytes, int d)
@@ -2573,8 +2632,11 @@ __global__ __launch_bounds__(kBlock) void xpack_kernel(XArgs t)
          k += (unsigned long long)gridDim.y * blockDim.x)
         dst[k] = ring[(r0 + k) & (t.outbox_cap - 1)];
     if (blockIdx.y == 0 && threadIdx.x == 0) {
+        // (the consumed position becomes visible to the expand kernel, which may
+        // run beside this launch and reuses ring places up to it, only once every
+        // block of this launch has copied its records out: the insert kernel that
+        // follows on this stream publishes it)
         x->r[par ^ 1][d] = r0 + n;
-        st_agent(&x->r_pub[d], r0 + n);
         XHdr h{};
         h.n = n;
         h.sent_all = sent_all;
@@ -2663,6 +2725,9 @@ __global__ __launch_bounds__(kBlock) void xinsert_kernel(SearchArgs a, XArgs t)
         goal_s = (int)goal;
         if (blockIdx.x == 0) {
             XState *x = t.x;
+            // the ring places this step's pack kernel has copied out are free now
+            for (int d = 0; d < G; d++)
+                st_agent(&x->r_pub[d], x->r[(t.step & 1) ^ 1][d]);
             x->received += tot;
             if (demand > x->demand_max)
                 x->demand_max = demand;
@@ -2730,7 +2795,8 @@ __global__ __launch_bounds__(kBlock) void xinsert_kernel(SearchArgs a, XArgs t)
             valid = g + h < bound;
         }
         route_child<KW, 1, false>(a, P, st, f0, w, valid, true, P.shard, ck, g, h, m, claimed, ovf,
-                                  LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr}, true);
+                                  LocalPush<KW>{nullptr, nullptr, 0, 0, nullptr, nullptr, t.stage, t.stage_n, t.stage_cap},
+                                  true);
     }
     claimed = wave_sum(claimed);
     ovf = wave_sum(ovf);

@@ -277,6 +277,12 @@ struct pastar_ctx {
     DevBuf<XState> xstate;
     DevBuf<StepStats> stats_b;         // the insert kernel's step statistics
     DevBuf<unsigned char> xsend, xrecv;  // [2][G] and [G] blocks of xblock_bytes
+    // xchg_lag = 1: the open-list entries of the records an insert received, by step parity, appended by
+    // xdrain_kernel on the main stream; their counts [2], the drain launch's arrival counter
+    DevBuf<Entry> xstage;
+    DevBuf<unsigned long long> xstage_n;
+    DevBuf<unsigned> xdrain_arrive;
+    size_t xstage_cap = 0;  // entries per parity
     // the exchange block in use (sized per round from the demand seen, up
     // to the allocated maximum) and the fixed stride between the send areas
     unsigned long long xblock_bytes = 0, xblock_recs = 0, xblock_recs_max = 0, xarea = 0;
@@ -1681,6 +1687,21 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         // lag 0: the next select sees this step's received records; lag 1: it
         // runs beside their exchange and insert (they reach the select after).
         const int lag = cfg.xlag;
+        if (lag) {
+            // the staging arrays of the inserts that run beside a select
+            const size_t cap = (size_t)G * (size_t)c->xblock_recs_max;
+            if (c->xstage_cap < cap) {
+                c->xstage.reset();
+                PA_TRY(c->xstage.alloc(2 * cap));
+                c->xstage_cap = cap;
+            }
+            if (!c->xstage_n.p) {
+                PA_TRY(c->xstage_n.alloc(2));
+                PA_TRY(c->xdrain_arrive.alloc(1));
+            }
+            HIP_TRY(hipMemsetAsync(c->xstage_n.p, 0, 2 * sizeof(unsigned long long), c->stream));
+            HIP_TRY(hipMemsetAsync(c->xdrain_arrive.p, 0, sizeof(unsigned), c->stream));
+        }
         XArgs t{};
         t.x = c->xstate.p;
         t.ctl = c->ctl.p;
@@ -1730,6 +1751,16 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 const int ring = (int)(step % kEvRing);
                 if (step - 1 - lag >= 0)
                     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_b[(step - 1 - lag) % kEvRing], 0));
+                if (lag && step - 2 >= 0) {
+                    // the entries insert(step - 2) staged (same parity as this step), into the
+                    // open list on this stream, before this step's select
+                    SearchArgs ad = a;
+                    ad.lower = &c->ctl.p->low_b;
+                    hipLaunchKernelGGL(xdrain_kernel, dim3(64), blk, 0, c->stream, ad,
+                                       c->xstage.p + (size_t)(step & 1) * c->xstage_cap, c->xstage_n.p + (step & 1),
+                                       (unsigned long long)c->xstage_cap, c->xdrain_arrive.p);
+                    PA_TRY(check_launch());
+                }
                 a.step = (int)(step & 0x3fffffff);
                 hipLaunchKernelGGL(select_kernel, dim3(1), blk, 0, c->stream, a);
                 ops.expand(expand_grid, blk, c->stream, a);
@@ -1738,6 +1769,11 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 HIP_TRY(hipStreamWaitEvent(c->stream_b, c->ev_a[ring], 0));
                 t.step = a.step;
                 t.send = c->xsend.p + (size_t)(step & 1) * c->xarea;
+                if (lag) {
+                    t.stage = c->xstage.p + (size_t)(step & 1) * c->xstage_cap;
+                    t.stage_n = c->xstage_n.p + (step & 1);
+                    t.stage_cap = (unsigned long long)c->xstage_cap;
+                }
                 ops.xpack(dim3((unsigned)G, pack_y), blk, c->stream_b, t);
                 PA_TRY(check_launch());
                 PA_TRY(c->tr->xchg(c, (int)(step & 0x3fffffff)));
