@@ -735,6 +735,85 @@ __device__ __forceinline__ int2 child_cost(const DevProblem &P, int npairs, cons
     return make_int2(dg, hh);
 }
 
+// ---------------------------------------------------------------------------
+// Split tables for wide fan-outs (fixed N >= 7, one parent per wave).  A
+// child's cost is a sum over all P pairs of the term its mask selects, 28
+// LDS reads a child for N = 8, times 255 children.  With the sequences split
+// into a low half (NL = N / 2 of them) and a high half, m = m_hi << NL | m_lo,
+//   cost(m) = A[m_lo] + B[m_hi] + sum over y in the high half of D[y][bit y of m][m_lo]
+// where A and B hold the pairs inside one half and D[y][b][m_lo] the NL pairs
+// of y with the low half: 1 + NH + 1 reads a child, from tables of
+// 2^NL + 2^NH + 2 NH 2^NL entries that the wave builds once per parent out of
+// the staged terms (160 entries for N = 8, 704 term reads for 7140).  Integer
+// sums in another order: the same values.
+// ---------------------------------------------------------------------------
+template <int N>
+struct SplitCost {
+    static constexpr int NL = N / 2, NH = N - NL;
+    static constexpr int kA = 0, kB = 1 << NL, kD = kB + (1 << NH);
+    static constexpr int kEntries = kD + 2 * NH * (1 << NL);
+    __host__ __device__ static constexpr int pair_index(int x, int y) { return x * (2 * N - x - 1) / 2 + (y - x - 1); }
+};
+
+// Builds the wave's tables `tab` (SplitCost<N>::kEntries int2) from its staged
+// terms; every lane of the wave calls it, and waits for LDS before reading.
+template <int N>
+__device__ __forceinline__ void split_cost_build(const int2 *terms, int2 *tab, int lane)
+{
+    using S = SplitCost<N>;
+    for (int e = lane; e < S::kEntries; e += 64) {
+        int dg = 0, hh = 0;
+        if (e < S::kD) {
+            // pairs inside one half: the low half's by m_lo, the high half's by m_hi
+            const bool hi = e >= S::kB;
+            const int bits = hi ? e - S::kB : e, off = hi ? S::NL : 0, cnt = hi ? S::NH : S::NL;
+#pragma unroll
+            for (int xl = 0; xl < S::NH - 1; xl++) {
+#pragma unroll
+                for (int yl = xl + 1; yl < S::NH; yl++) {
+                    if (yl < cnt) {
+                        const int x = xl + off, y = yl + off;
+                        const int p = x * (2 * N - x - 1) / 2 + (y - x - 1);
+                        const int c = (((bits >> xl) & 1) << 1) | ((bits >> yl) & 1);
+                        const int2 t = terms[p * 4 + c];
+                        dg += t.x;
+                        hh += t.y;
+                    }
+                }
+            }
+        } else {
+            // y of the high half against every x of the low half
+            const int k = e - S::kD, mlo = k & ((1 << S::NL) - 1), by = (k >> S::NL) & 1, y = S::NL + (k >> (S::NL + 1));
+#pragma unroll
+            for (int x = 0; x < S::NL; x++) {
+                const int p = x * (2 * N - x - 1) / 2 + (y - x - 1);
+                const int c = (((mlo >> x) & 1) << 1) | by;
+                const int2 t = terms[p * 4 + c];
+                dg += t.x;
+                hh += t.y;
+            }
+        }
+        tab[e] = make_int2(dg, hh);
+    }
+}
+
+// (delta g, h) of the child with mask m from the wave's split tables.
+template <int N>
+__device__ __forceinline__ int2 split_cost(const int2 *tab, int m)
+{
+    using S = SplitCost<N>;
+    const int mlo = m & ((1 << S::NL) - 1), mhi = m >> S::NL;
+    const int2 a = tab[S::kA + mlo], b = tab[S::kB + mhi];
+    int dg = a.x + b.x, hh = a.y + b.y;
+#pragma unroll
+    for (int yl = 0; yl < S::NH; yl++) {
+        const int2 d = tab[S::kD + ((yl * 2 + ((mhi >> yl) & 1)) << S::NL) + mlo];
+        dg += d.x;
+        hh += d.y;
+    }
+    return make_int2(dg, hh);
+}
+
 template <int N, int KW, typename PP>
 __device__ __forceinline__ void child_key(const PP &P, int n, const uint64_t (&key)[KW], int m,
                                           uint64_t (&out)[KW])

@@ -1371,6 +1371,9 @@ __device__ __forceinline__ Entry batch_entry_at(const SearchArgs &a, const SelVi
 #ifndef PASTAR_DIVE
 #define PASTAR_DIVE 1
 #endif
+#ifndef PASTAR_SPLIT_COST
+#define PASTAR_SPLIT_COST 1
+#endif
 #ifndef PASTAR_DIVE_W
 #define PASTAR_DIVE_W 6
 #endif
@@ -1459,6 +1462,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         child_key<N, KW>(P, n, zero, kTwoLevel ? wave * npw + group : 0, kinc_grp);
     }
     __shared__ int2 terms_all[kWaves][terms_per_wave(N)];
+    // wide fan-outs with one parent per wave: a child's cost from split tables (device.hpp, SplitCost)
+    constexpr bool kSplit = PASTAR_SPLIT_COST && N >= 7;
+    __shared__ int2 split_all[kSplit ? kWaves : 1][kSplit ? SplitCost<N ? N : 8>::kEntries : 1];
     // batch offsets fit 32 bits (batch_nodes <= 2^30, checked on the host)
     __shared__ uint32_t prefix[kRanges + 1];
     __shared__ unsigned long long bstart[kRanges];
@@ -1655,6 +1661,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         // a wave reads only the terms it staged itself (terms_all[wave]):
         // its own LDS writes landing is enough, no block barrier
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (kSplit) {
+            // (one parent per wave: the wave's tables, built from its terms)
+            if (__ballot(ok)) {  // uniform
+                split_cost_build<N>(terms, split_all[wave], lane);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
         BPHASE(2)
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
@@ -1665,7 +1678,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             for (int k = 0; k < KW; k++)
                 ck[k] = 0;
             if (valid) {
-                const int2 dc = child_cost<N>(Pg, npairs, terms, m);
+                int2 dc;
+                if constexpr (kSplit)
+                    dc = split_cost<N>(split_all[wave], m);
+                else
+                    dc = child_cost<N>(Pg, npairs, terms, m);
                 g = par_.g + dc.x;
                 h = dc.y;
                 const int f = g + h;
