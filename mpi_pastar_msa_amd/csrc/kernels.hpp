@@ -1669,6 +1669,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             }
         }
         BPHASE(2)
+        // several rounds of 64 masks: the key of this lane's child is the
+        // parent's plus the increments of the mask's low six bits, the lane's
+        // and the same in every round, plus those of its high bits, the
+        // round's and the same on every lane
+        uint64_t klane[KW];
+        if constexpr (!kOneRound && N > 0)
+            child_key<N, KW>(P, n, par_.key, glane, klane);
         for (int r = 0; r * lpn < masks; r++) {
             const int m = r * lpn + glane;
             bool valid = ok && m >= 1 && m < masks && !(m & par_.blocked);
@@ -1701,6 +1708,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
 #pragma unroll
                     for (int k = 0; k < KW; k++)
                         ck[k] = par_.key[k] + kinc[k];
+                } else if constexpr (N > 0) {
+                    const uint64_t zero[KW] = {};
+                    uint64_t rinc[KW];
+                    child_key<N, KW>(P, n, zero, r * lpn, rinc);  // (uniform)
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        ck[k] = klane[k] + rinc[k];
                 } else {
                     child_key<N, KW>(P, n, par_.key, m, ck);
                 }
