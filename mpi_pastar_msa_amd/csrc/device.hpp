@@ -209,6 +209,31 @@ __device__ __forceinline__ unsigned long long bcast_lane(unsigned long long v, i
     return ((unsigned long long)hi << 32) | lo;
 }
 
+// Wave-wide reductions on DPP lane moves (no LDS round trip): an inclusive
+// row scan (row_shr 1, 2, 4, 8), then row_bcast 15 and 31; lane 63 holds the
+// total.  Every lane of the wave must be active.
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_dpp(int v, int identity, Op op)
+{
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x111, 0xf, 0xf, false));
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x112, 0xf, 0xf, false));
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x114, 0xf, 0xf, false));
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x118, 0xf, 0xf, false));
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x142, 0xa, 0xf, false));
+    v = op(v, __builtin_amdgcn_update_dpp(identity, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ int wave_min_i32(int v)
+{
+    return wave_reduce_dpp(v, kIntMax, [](int x, int y) { return x < y ? x : y; });
+}
+
+__device__ __forceinline__ int wave_sum_i32(int v)
+{
+    return wave_reduce_dpp(v, 0, [](int x, int y) { return x + y; });
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x)
 {
     x ^= x >> 33;

@@ -1734,12 +1734,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
         if constexpr (kPartial) {
             if (partial_k >= 0) {  // uniform
                 // the parent again, under the lowest f it has left
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_xor(pend_f, o);
-                    if (o < lpn)
-                        pend_f = y < pend_f ? y : pend_f;
-                }
+                // (one parent per wave wherever this is compiled in: a DPP reduction, no LDS round trips)
+                pend_f = wave_min_i32(pend_f);
                 // (queued `partial_ahead` buckets before its first child is
                 // due, but past this batch: the children are then in their
                 // buckets before those are cut, not after; the entry keeps
