@@ -570,21 +570,32 @@ struct SearchArgs {
     unsigned long long maxch, pool_chunks;
 };
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+// (DPP lane moves, no LDS round trips; every lane of the wave must be active)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void wave_sum_step64(unsigned &lo, unsigned &hi)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o);
-    return v;
+    const unsigned l2 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROW_MASK, 0xf, false);
+    const unsigned h2 = (unsigned)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROW_MASK, 0xf, false);
+    const unsigned long long t = (((unsigned long long)hi << 32) | lo) + (((unsigned long long)h2 << 32) | l2);
+    lo = (unsigned)t;
+    hi = (unsigned)(t >> 32);
 }
 
-__device__ __forceinline__ unsigned wave_sum(unsigned v)
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o);
-    return v;
+    // an inclusive row scan (row_shr 1, 2, 4, 8), then row_bcast 15 and 31: lane 63 holds the total
+    unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+    wave_sum_step64<0x111, 0xf>(lo, hi);
+    wave_sum_step64<0x112, 0xf>(lo, hi);
+    wave_sum_step64<0x114, 0xf>(lo, hi);
+    wave_sum_step64<0x118, 0xf>(lo, hi);
+    wave_sum_step64<0x142, 0xa>(lo, hi);
+    wave_sum_step64<0x143, 0xc>(lo, hi);
+    const unsigned tl = (unsigned)__builtin_amdgcn_readlane((int)lo, 63), th = (unsigned)__builtin_amdgcn_readlane((int)hi, 63);
+    return ((unsigned long long)th << 32) | tl;
 }
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) { return (unsigned)wave_sum_i32((int)v); }
 
 // Wave-aggregated append to a destination's outbox ring: one atomic per wave
 // on the ring's append position; a record that would overrun what the pack
