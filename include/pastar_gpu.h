@@ -41,7 +41,7 @@ extern "C" {
 #endif
 
 #define PASTAR_MAX_SEQ 16
-#define PASTAR_ABI_VERSION 3
+#define PASTAR_ABI_VERSION 4
 
 /* status codes */
 #define PASTAR_OK 0
