@@ -1880,7 +1880,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
             int org[N];
             LEntry<KW> mine{};
             int mpos[N];
-            constexpr bool elig = true;
             if (dive) {  // uniform
                 const int li = lane & (kDiveFront - 1);
                 mine = lq[cur][li < cnt ? li : 0];
@@ -1962,7 +1961,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                 // (no block barrier inside): each of its lane groups holds
                 // one node of the level, lane m of the group its child m
                 if (wave == 0) {
-                    const LocalPush<KW> lq_back{lq[nxt], &lq_count[nxt], f_limit, lq_cap, outq, &out_n};
                     bool okp = false;
                     int nrel = 0;
                     if (starter) {
@@ -1970,7 +1968,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                         const bool okb = mine.g + mine.h < bound;
                         okp = okb && (uint32_t)(sbest >> 32) >= (uint32_t)mine.g;
                         stale += okb && !okp;
-                        if (okp && elig) {
+                        if (okp) {
                             reopen += (int)(uint32_t)saux != kIntMax;
                             *(int *)(a.table + (uint64_t)mine.slot * SW + KW + 1) = mine.g;
                             expanded++;
@@ -1980,13 +1978,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(expand_w
                             atomicMin(&relbest[rel_index(nrel)], mine.g);
                         }
                     }
-                    // (a current node outside the window: back into the queue as it is)
-                    {
-                        const uint64_t bk[KW] = {mine.key[0]};
-                        queue_improved<KW>(a, st, f0, w, starter && okp && !elig, mine.slot, bk, mine.g, mine.h, mine.pmask,
-                                           lq_back);
-                    }
-                    okp = okp && elig;
                     // this lane's child: its mask's constants
                     const int m = glane;
                     const int relinc = (m & 1) | ((m >> 1) & 1) << 4 | ((m >> 2) & 1) << 8 | ((m >> 3) & 1) << 12;
