@@ -463,7 +463,8 @@ struct Ctl {
     int partial_k;    // partial expansion: children with f at or past the batch's last bucket + this many buckets
                       // wait until their parent is taken again (negative: every child at once)
     int partial_ahead;  // that parent is queued this many buckets before its first waiting child's
-    int partial_two;    // 1: a parent taken again generates every child it has left
+    int partial_two;    // a parent taken again: 1 (default) generates every child it has left; 0 the same window
+                        // again; 2 a window that doubles its reach past the parent's f (tuning probes)
     unsigned long long kmax;
     unsigned long long pool_chunks, maxch;
     unsigned long long table_slots;
