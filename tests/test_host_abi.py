@@ -46,6 +46,24 @@ def test_abi_version():
     assert nat.lib().pastar_abi_version() == version
 
 
+def test_search_opts_layout_matches_header():
+    """The ctypes mirror of pastar_search_opts has the header's fields in the
+    header's order (the options travel by value across the C-ABI), and the
+    Python options land in the fields of the same name."""
+    from mpi_pastar_msa_amd import PAStarOpt
+    text = open(HEADER).read()
+    body = re.search(r"typedef struct pastar_search_opts \{(.*?)\} pastar_search_opts;", text, flags=re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    declared = re.findall(r"\b(int64_t|int32_t)\s+([a-z_0-9]+);", body)
+    mirror = [(name, ctype) for name, ctype in nat.pastar_search_opts._fields_]
+    assert [n for _, n in declared] == [n for n, _ in mirror]
+    for (ctype_name, name), (_, ctype) in zip(declared, mirror):
+        assert ctypes.sizeof(ctype) == (8 if ctype_name == "int64_t" else 4), name
+    so = PAStarOpt(partial=3, xchg_lag=1, depth=7, batch_nodes=99, band=5, xchg_block_records=4096).search_opts()
+    assert (so.partial, so.xchg_lag, so.depth, so.batch_nodes, so.band, so.xchg_block_records) == (3, 1, 7, 99, 5, 4096)
+    assert PAStarOpt().search_opts().partial == 0  # the engine's default: partial expansion on for N >= 7
+
+
 @pytest.mark.skipif(HAS_GPU, reason="a GPU is present")
 def test_device_entry_points_fail_loudly_without_gpu():
     from mpi_pastar_msa_amd import Engine
