@@ -479,9 +479,11 @@ def main():
     if gen and exp_local and launches and not results[-1][0].solo:
         # the same fraction with the children the kernel did relax in place of the reference's 2^N - 1 per
         # expansion (partial expansion for N >= 7 leaves most of them ungenerated; border nodes have fewer)
+        # (capped at 2^N - 1: the dive also relaxes the children of nodes whose expansion did not count)
         s_rec = 2 * n + 12
-        b_rel = s_rec + 16 * (n * (n - 1) // 2) + n + 2 * (gen / exp_local) * s_rec
-        roof["children_relaxed_per_expansion"] = gen / exp_local
+        kids = min(gen / exp_local, float((1 << n) - 1))
+        b_rel = s_rec + 16 * (n * (n - 1) // 2) + n + 2 * kids * s_rec
+        roof["children_relaxed_per_expansion"] = kids
         roof["frac_children_relaxed"] = (exp_local / launches) * b_rel / avg_launch_s / 1e9 / HBM_PEAK_GBS
     if kern_ms > 0 and gen and not results[-1][0].solo:
         # the random-access view of the same kernel: every generated child
