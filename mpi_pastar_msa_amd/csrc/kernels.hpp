@@ -3098,53 +3098,54 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
     walk_chain<N, KW>(Pp, table, cap_mask, start, max, local_only, masks, last_key, info);
 }
 
-// The backtrace walk two steps per memory round trip (one shard, 1-word keys,
-// 2 <= N <= 6; same result as walk_kernel with local_only = 0).  One wave:
-// lane 0 fetches the first probe line of the current node, and lane m
-// (1 <= m < 2^N) that of the node's candidate parent node - m.  The round
-// trip that returns the node's parent mask m0 then also holds the parent's
-// record (lane m0's line) and so the parent's own mask: the grandparent is
-// the next round's node.  A record missing from its first line (a displaced
-// key, rare at the table's load) is looked up along its probe chain.
+// The backtrace walk many steps per memory round trip (one shard, 1-word
+// keys, 2 <= N <= 6; same result as walk_kernel with local_only = 0).  Most
+// columns of an alignment hold no gap: their parent mask steps back in every
+// sequence at once.  One wave: lane j fetches the first probe line of the node
+// j such steps behind the current one (lane 0: the node itself).  The records
+// that came back tell in one ballot how far the path keeps to that diagonal;
+// the first record with another mask, if it is at hand, is the round's last
+// step, and the next round starts from where it leads.  Nothing in a round
+// is serial but the one memory latency (~0.5 us): no step-by-step chain (a
+// store and a dependent broadcast per step cost 160 ns each), and every
+// lane's mask goes out in one store.  A node missing from its first line (a
+// displaced key, rare at the table's load) is looked up along its probe
+// chain when it is the round's first, and ends the round before it otherwise.
 template <int N>
 __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
                                             uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
                                             int32_t *__restrict__ masks, uint64_t *__restrict__ last_key,
-                                            int *__restrict__ info)
+                                            int *__restrict__ info, unsigned long long *dbg = nullptr)
 {
-    static_assert(N >= 2 && N <= 6, "one lane per candidate parent");
+    static_assert(N >= 2 && N <= 6, "fixed N, 1-word keys");
+#ifdef PASTAR_PHASE_TIMERS
+    const unsigned long long w_t0 = device_clock();
+    unsigned long long w_t1 = 0, w_t2 = 0, w_rounds = 0, w_fetch = 0;
+#endif
     constexpr int SW = slot_words<1>();
     constexpr int LS = line_slots<1>();
+    constexpr uint32_t kFull = (1u << N) - 1;  // the mask of a step back in every sequence at once
     const DevProblem &Pg = *Pp;
     const KConst<N, 1> P = load_kconst<N, 1>(Pg);
     const int lane = lane_id();
-    // this lane's key decrement (its candidate's coordinate offsets)
-    uint64_t dec = 0;
+    // one step back in every sequence, and this lane's `lane` of them
+    uint64_t diag = 0;
 #pragma unroll
     for (int i = 0; i < N; i++)
-        if ((lane >> i) & 1)
-            dec += 1ull << P.kshift[i];
+        diag += 1ull << P.kshift[i];
+    const uint64_t dec = diag * (uint64_t)lane;
     const uint64_t origin = Pg.origin_key[0];
     uint64_t key = start[0];  // uniform
     int steps = 0, status = 0;
-    // best of `k` along its whole probe chain (uniform; the rare path)
-    auto full_best = [&](uint64_t k, uint64_t &best) -> bool {
-        const uint64_t kk[1] = {k};
-        const int64_t s = lookup<1>(table, cap_mask, kk);
-        if (s < 0)
-            return false;
-        best = table[(uint64_t)s * SW + 1];
-        return true;
-    };
-    // the uniform key decrement of mask m
-    auto step_back = [&](uint64_t k, int m) -> uint64_t {
-#pragma unroll
-        for (int i = 0; i < N; i++)
-            if ((m >> i) & 1)
-                k -= 1ull << P.kshift[i];
-        return k;
-    };
-    for (;;) {
+    while (status == 0) {
+#ifdef PASTAR_PHASE_TIMERS
+        if (w_rounds == 0)
+            w_t1 = device_clock();
+        if (w_rounds == 1)
+            w_t2 = device_clock();
+        w_rounds++;
+        const unsigned long long w_r0 = device_clock();
+#endif
         if (key == origin) {
             status = 1;
             break;
@@ -3156,10 +3157,10 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
         int pos[N];
         const uint64_t kk[1] = {key};
         decode_key<N, 1>(P, N, kk, pos);
-        bool valid = lane < (1 << N);
+        bool valid = true;  // the node `lane` steps down the diagonal exists
 #pragma unroll
         for (int i = 0; i < N; i++)
-            if (((lane >> i) & 1) && pos[i] == 0)
+            if (pos[i] < lane)
                 valid = false;
         const uint64_t ck = key - dec;  // lane 0: the node itself
         uint64_t best = ~0ull;
@@ -3179,40 +3180,65 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
                     found = true;
                 }
         }
+        if (!(__ballot(found) & 1ull)) {  // (uniform; the rare path)
+            const int64_t s = lookup<1>(table, cap_mask, kk);
+            if (s < 0) {
+                status = -1;
+                break;
+            }
+            if (lane == 0) {
+                best = table[(uint64_t)s * SW + 1];
+                found = true;
+            }
+        }
+#ifdef PASTAR_PHASE_TIMERS
+        if (w_rounds > 1)
+            w_fetch += device_clock() - w_r0;
+#endif
+        const uint32_t m = (uint32_t)best;  // the parent mask of this lane's node
         const uint64_t hit = __ballot(found);
-        uint64_t b0 = bcast_lane((unsigned long long)best, 0);
-        if (!(hit & 1ull) && !full_best(key, b0)) {
-            status = -1;
-            break;
+        // (the origin's record carries the full mask too: it has no parent)
+        const uint64_t full = __ballot(found && m == kFull && ck != origin);
+        // (uniform from here) the run of full steps from the node on; it ends
+        // at the origin at the latest
+        const int run = full == ~0ull ? 64 : __builtin_ctzll(~full);
+        int count = run;
+        uint64_t next = key - diag * (uint64_t)run;
+        if (next != origin && run < 64 && ((hit >> run) & 1ull)) {
+            // the record that ends the run is at hand: the round's last step
+            const uint32_t ml = (uint32_t)bcast_lane((int)m, run);
+            if (ml == 0 || ml > kFull) {
+                status = -1;  // no such parent
+                break;
+            }
+            count++;
+#pragma unroll
+            for (int i = 0; i < N; i++)
+                if ((ml >> i) & 1)
+                    next -= 1ull << P.kshift[i];
         }
-        const int m0 = (int)(uint32_t)b0;
-        if (lane == 0)
-            masks[steps] = m0;
-        steps++;
-        key = step_back(key, m0);
-        if (key == origin) {
-            status = 1;
-            break;
-        }
-        if (steps >= max) {
+        if (steps + count > max) {
             status = 2;
             break;
         }
-        uint64_t b1 = bcast_lane((unsigned long long)best, m0 & 63);
-        if (!((hit >> (m0 & 63)) & 1ull) && !full_best(key, b1)) {
-            status = -1;
-            break;
-        }
-        const int m1 = (int)(uint32_t)b1;
-        if (lane == 0)
-            masks[steps] = m1;
-        steps++;
-        key = step_back(key, m1);
+        if (lane < count)
+            masks[steps + lane] = (int32_t)m;
+        steps += count;
+        key = next;
     }
     if (lane == 0) {
         last_key[0] = key;
         info[0] = steps;
         info[1] = status;
+#ifdef PASTAR_PHASE_TIMERS
+        if (dbg) {  // diagnostics: set-up, the first round trip, the rest (device clock ticks), round trips
+            dbg[0] = w_t1 - w_t0;
+            dbg[1] = w_t2 - w_t1;
+            dbg[2] = device_clock() - w_t2;
+            dbg[10] = w_rounds;
+            dbg[12] = w_fetch;  // of the rest: a round's start to its records' arrival
+        }
+#endif
     }
 }
 
@@ -3288,11 +3314,19 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
         }
         return;
     }
+#ifdef PASTAR_PHASE_TIMERS
+    const unsigned long long tail_t0 = device_clock();
+#endif
     if (blockIdx.x == 0) {
         if (threadIdx.x < 64) {
             constexpr bool kTwo = KW == 1 && N >= 2 && N <= 6;
             if constexpr (kTwo)
+#ifdef PASTAR_PHASE_TIMERS
+                walk2_chain<kTwo ? N : 2>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key, t.info,
+                                          t.h_census + 5);
+#else
                 walk2_chain<kTwo ? N : 2>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key, t.info);
+#endif
             else if (threadIdx.x == 0)
                 walk_chain<N, KW>(t.P, t.table, t.cap_mask, t.goal_key, t.max, 0, t.masks, t.last_key, t.info);
         }
@@ -3307,6 +3341,13 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
     }
     __shared__ int last;
     __syncthreads();
+#ifdef PASTAR_PHASE_TIMERS
+    const unsigned long long tail_t1 = device_clock();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // diagnostics: the walk's start and end
+        t.h_census[13] = tail_t0;
+        t.h_census[14] = tail_t1;
+    }
+#endif
     if (threadIdx.x == 0) {
         __threadfence();  // the walk's masks and info, the census adds: visible to the last block
         last = atomicAdd(t.arrive, 1u) == gridDim.x - 1;
@@ -3315,6 +3356,15 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
     if (!last)
         return;
     __threadfence();
+#ifdef PASTAR_PHASE_TIMERS
+    // diagnostics: the last block's start, its work done, the fences passed, the copies issued (device clock ticks)
+    if (threadIdx.x == 0) {
+        t.h_census[8] = tail_t0;
+        t.h_census[9] = tail_t1;
+        t.h_census[10] = device_clock();
+        t.h_census[12] = blockIdx.x;
+    }
+#endif
     tail_copy_ctl(t);
     if (threadIdx.x < 5)
         t.h_census[threadIdx.x] = ld_agent(&t.census[threadIdx.x]);
@@ -3326,6 +3376,10 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
         t.h_masks[k] = ld_agent(&t.masks[k]);
     if (threadIdx.x == 0)
         *t.arrive = 0;
+#ifdef PASTAR_PHASE_TIMERS
+    if (threadIdx.x == 0)
+        t.h_census[11] = device_clock();
+#endif
     tail_done(t);
 }
 

@@ -1957,6 +1957,17 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         std::fprintf(stderr, "[pastar] dives %llu (one start node %llu, several %llu), levels %llu, by levels 0: %llu 1: %llu "
                      "2: %llu 3+: %llu, children %llu\n", h.body_ticks[10], h.phase_ticks[0], h.phase_ticks[1], h.body_ticks[11],
                      h.phase_ticks[4], h.phase_ticks[5], h.phase_ticks[6], h.phase_ticks[7], h.phase_ticks[2]);
+#ifdef PASTAR_PHASE_TIMERS
+        if (!sharded)
+            std::fprintf(stderr, "[pastar] tail (us): walk %.2f; last block %llu: own work %.2f, arrival and fences %.2f, "
+                         "copies to the host %.2f; walk's start to the copies' end %.2f\n", (double)(cz[14] - cz[13]) * 1e-2,
+                         cz[12], (double)(cz[9] - cz[8]) * 1e-2, (double)(cz[10] - cz[9]) * 1e-2,
+                         (double)(cz[11] - cz[10]) * 1e-2, (double)(cz[11] - cz[13]) * 1e-2);
+        if (!sharded)
+            std::fprintf(stderr, "[pastar] walk (us): set-up %.2f, first round trip %.2f, the other %llu %.2f, of which "
+                         "%.2f from a round's start to its records' arrival\n", (double)cz[5] * 1e-2, (double)cz[6] * 1e-2,
+                         cz[15] > 1 ? cz[15] - 2 : 0ull, (double)cz[7] * 1e-2, (double)cz[17] * 1e-2);
+#endif
     }
     res->gap_ms = (double)h.gap_ticks * 1e-5;
     res->expand_launches = launches;
