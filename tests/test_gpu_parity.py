@@ -200,6 +200,37 @@ def test_random_small_problems_match_oracle(mode):
             assert o.alignment_cost(rows) == ref["score"]
 
 
+@pytest.mark.parametrize("eager", [False, True])
+def test_backtrace_walk_shapes(eager):
+    """The backtrace walk looks up to 64 nodes down the diagonal per round:
+    alignments without a gap over more than 64 columns (identical sequences),
+    long runs of gap columns at either end, N = 2 and N = 6, a sequence of
+    one residue; behind a graph replay (the replay tail) and after eager
+    launches (the walk's own launch)."""
+    rng = random.Random(31)
+    alphabet = "ACDEFGHIKLMNPQRSTVWY"
+
+    def rnd(k):
+        return "".join(rng.choice(alphabet) for _ in range(k))
+
+    core = rnd(150)
+    cases = [[core, core], [core, core, core], [core[:64], core[:64]], [core[:65], core[:65], core[:65]],
+             [rnd(30) + core[:80] + rnd(20), core[:80]], [core[:70], rnd(25) + core[:70]],
+             [core[:90], core[:40] + core[50:90], core[:90]],
+             [rnd(rng.randint(3, 9)) for _ in range(6)], [core[:40], "W", core[:40], core[1:40]]]
+    for seqs in cases:
+        o = orc.Oracle(seqs=seqs)
+        ref = o.astar()
+        with Engine(seqs).init() as e:
+            r = e.pa_star(PAStarOpt(mode="batched", eager=eager))
+            assert r.score == ref["score"] and r.solo == 0, (seqs, r, ref)
+            rows = e.alignment()
+            assert [row.replace("-", "") for row in rows] == seqs
+            assert o.alignment_cost(rows) == ref["score"]
+            if seqs[0] == seqs[-1] and len(set(seqs)) == 1:
+                assert rows == seqs  # no gap at all
+
+
 @pytest.mark.parametrize("mode", ["batched", "auto"])
 def test_random_edge_problems_match_oracle(mode):
     """Edge shapes: 7 and 8 sequences (the multi-round child loop with 1-word
