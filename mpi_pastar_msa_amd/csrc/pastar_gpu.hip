@@ -416,6 +416,17 @@ int setup_problem(pastar_ctx *c, const pastar_problem *p)
                 c->weights.push_back((int)wf[(size_t)x * c->n + y]);
     }
 
+    // (the reference's weighting gives negative pair weights to some families
+    // of near-identical sequences, WeightedSP.cpp:464-509, and searches with
+    // them all the same: h is then no lower bound, and which alignment A*
+    // ends with depends on the order of expansion, in the reference too)
+    for (int k = 0; k < c->npairs; k++)
+        if (c->weights[(size_t)k] < 0) {
+            std::fprintf(stderr, "[pastar] warning: pair weight %d is negative (%d): the heuristic is no lower bound, "
+                         "the alignment returned need not be optimal\n", k, c->weights[(size_t)k]);
+            break;
+        }
+
     DevProblem &hp = c->hp;
     std::memset(&hp, 0, sizeof(hp));
     hp.n = c->n;

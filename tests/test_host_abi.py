@@ -117,6 +117,20 @@ def test_weights_random_sets_bit_exact():
         assert compute_weights(seqs).tobytes() == orc.weights(seqs).tobytes()
 
 
+def test_weights_degenerate_families_follow_oracle():
+    """Families of near-identical sequences on which the reference's weighting
+    (WeightedSP.cpp:464-509) turns negative, or divides by a smallest weight
+    of zero: the host pipeline gives the oracle's bits there too (the search
+    over such weights has no defined optimum, in the reference either)."""
+    neg = ["NTARICGENSIPVWIAHQKGPNDFYYRAFAAH", "SIPVEWIAHQHKGPGDFYYRFFAAH", "NTARICCENSIWPVEWIAHQKGGPRGDFY",
+           "NTARICGENSIPVEWIAHQGPGDFYYRFFAAH"]
+    nonfinite = ["EYKKIRYLAMTPHQV", "EYKKIRYLAMTPNQ", "EYKKIRYLAMWTPHQV"]
+    for seqs in (neg, nonfinite):
+        w, ref = compute_weights(seqs), orc.weights(seqs)
+        assert w.tobytes() == ref.tobytes()
+    assert (orc.weights(neg) < 0).any() and not np.isfinite(orc.weights(nonfinite)).all()
+
+
 def test_fasta_reader_matches_oracle(tmp_path):
     p = tmp_path / "q.fasta"
     p.write_bytes(b">a\nACD\nEF\n\nGH\n>b\r\nKLM\r\n>c\nNP")
