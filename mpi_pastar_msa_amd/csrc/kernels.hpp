@@ -3275,22 +3275,24 @@ struct TailArgs {
     unsigned long long *census;
     const Ctl *ctl;
     const int *goal;
-    unsigned *arrive;  // zero between launches
+    unsigned *arrive;  // [0] zero between launches; [1] tail launches so far (the completion word's value)
     Ctl *h_ctl;
     int *h_goal;
     unsigned long long *h_census;
     int *h_info;
     int32_t *h_masks;
-    uint32_t *h_done;  // set to `ticket` after everything above is in host memory
-    uint32_t ticket;
+    uint32_t *h_done;  // set to the launch's number after everything above is in host memory
 };
 
 __device__ __forceinline__ void tail_done(const TailArgs &t)
 {
     __syncthreads();  // the block's host writes issued
     if (threadIdx.x == 0) {
+        // (one thread per launch comes here, launches run in stream order)
+        const unsigned ticket = t.arrive[1] + 1;
+        t.arrive[1] = ticket;
         __threadfence_system();
-        __hip_atomic_store(t.h_done, t.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(t.h_done, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -1513,51 +1513,6 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                 ops.expand_one_shard(expand_grid, blk, c->stream, a);
             return hipGetLastError();
         };
-        bool use_graph = !cfg.eager;
-        std::vector<unsigned char> key(sizeof(SearchArgs) + 3 * sizeof(int));
-        {
-            std::memcpy(key.data(), &a, sizeof(SearchArgs));
-            const int extra[3] = {(int)expand_grid.x, c->n, KW};
-            std::memcpy(key.data() + sizeof(SearchArgs), extra, sizeof(extra));
-        }
-        if (use_graph && c->step_key != key) {  // new arguments: drop the runs captured for the old ones
-            for (int gi = 0; gi < kRuns; gi++) {
-                if (c->step_exec[gi])
-                    (void)hipGraphExecDestroy(c->step_exec[gi]);
-                if (c->step_graph[gi])
-                    (void)hipGraphDestroy(c->step_graph[gi]);
-                c->step_exec[gi] = nullptr;
-                c->step_graph[gi] = nullptr;
-            }
-            c->step_key = key;
-        }
-        // a run is captured the first time it is needed
-        auto run_exec = [&](int gi) -> hipGraphExec_t {
-            if (!use_graph || c->step_exec[gi])
-                return c->step_exec[gi];
-            hipGraph_t graph = nullptr;
-            hipGraphExec_t exec = nullptr;
-            hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
-            hipError_t e2 = e == hipSuccess ? enqueue_steps(kStepRuns[gi]) : e;
-            hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
-            if (e2 == hipSuccess && e3 == hipSuccess)
-                e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-            if (e2 != hipSuccess || e3 != hipSuccess) {
-                if (exec)
-                    (void)hipGraphExecDestroy(exec);
-                if (graph)
-                    (void)hipGraphDestroy(graph);
-                (void)hipGetLastError();
-                use_graph = false;
-                if (cfg.verbose)
-                    std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
-                                 hipGetErrorString(e2 != hipSuccess ? e2 : e3));
-                return nullptr;
-            }
-            c->step_graph[gi] = graph;
-            c->step_exec[gi] = exec;
-            return exec;
-        };
         long long steps_before = 0;
         int rc = PASTAR_OK;
         // the end-of-search work rides behind every replay, gated on the
@@ -1588,8 +1543,9 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         d_info += 8;  // h_walk[4..5]
         PA_TRY(host_alias(c->h_walk_masks, &d_masks));
         if (!c->tail_arrive.p) {
-            PA_TRY(c->tail_arrive.alloc(1));
-            HIP_TRY(hipMemsetAsync(c->tail_arrive.p, 0, sizeof(unsigned), c->stream));
+            PA_TRY(c->tail_arrive.alloc(2));  // arrival counter, ticket counter
+            HIP_TRY(hipMemsetAsync(c->tail_arrive.p, 0, 2 * sizeof(unsigned), c->stream));
+            c->tail_ticket = 0;
         }
         TailArgs ta{};
         ta.P = c->dP.p;
@@ -1614,32 +1570,89 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
         volatile uint32_t *done = reinterpret_cast<volatile uint32_t *>(reinterpret_cast<unsigned char *>(c->h_ctl) +
                                                                         sizeof(Ctl) + 32);
         ta.h_done = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(d_ctl) + sizeof(Ctl) + 32);
-        auto enqueue_tail = [&]() -> hipError_t {
-            ta.ticket = ++c->tail_ticket;
+        // (the ticket is counted on the device, in the word behind the arrival
+        // counter, one per tail launch like the host's: the launch's arguments
+        // never change, so a captured replay can hold it)
+        uint32_t ticket = 0;
+        auto expect_tail = [&]() {
+            ticket = ++c->tail_ticket;
             *done = 0;
+        };
+        auto enqueue_tail = [&]() -> hipError_t {
             ops.tail(c->stream, ta);
             return hipGetLastError();
         };
+        bool use_graph = !cfg.eager;
+        std::vector<unsigned char> key(sizeof(SearchArgs) + 3 * sizeof(int) + sizeof(TailArgs));
+        {
+            std::memcpy(key.data(), &a, sizeof(SearchArgs));
+            const int extra[3] = {(int)expand_grid.x, c->n, KW};
+            std::memcpy(key.data() + sizeof(SearchArgs), extra, sizeof(extra));
+            std::memcpy(key.data() + sizeof(SearchArgs) + sizeof(extra), &ta, sizeof(TailArgs));
+        }
+        if (use_graph && c->step_key != key) {  // new arguments: drop the runs captured for the old ones
+            for (int gi = 0; gi < kRuns; gi++) {
+                if (c->step_exec[gi])
+                    (void)hipGraphExecDestroy(c->step_exec[gi]);
+                if (c->step_graph[gi])
+                    (void)hipGraphDestroy(c->step_graph[gi]);
+                c->step_exec[gi] = nullptr;
+                c->step_graph[gi] = nullptr;
+            }
+            c->step_key = key;
+        }
+        // a run is captured the first time it is needed
+        auto run_exec = [&](int gi) -> hipGraphExec_t {
+            if (!use_graph || c->step_exec[gi])
+                return c->step_exec[gi];
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
+            hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+            hipError_t e2 = e == hipSuccess ? enqueue_steps(kStepRuns[gi]) : e;
+            if (e2 == hipSuccess) {  // the replay's tail is its last node (no gap between the last step and it)
+                ops.tail(c->stream, ta);
+                e2 = hipGetLastError();
+            }
+            hipError_t e3 = e == hipSuccess ? hipStreamEndCapture(c->stream, &graph) : e;
+            if (e2 == hipSuccess && e3 == hipSuccess)
+                e3 = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+            if (e2 != hipSuccess || e3 != hipSuccess) {
+                if (exec)
+                    (void)hipGraphExecDestroy(exec);
+                if (graph)
+                    (void)hipGraphDestroy(graph);
+                (void)hipGetLastError();
+                use_graph = false;
+                if (cfg.verbose)
+                    std::fprintf(stderr, "[pastar] graph capture refused (%s); eager launches\n",
+                                 hipGetErrorString(e2 != hipSuccess ? e2 : e3));
+                return nullptr;
+            }
+            c->step_graph[gi] = graph;
+            c->step_exec[gi] = exec;
+            return exec;
+        };
+
         // wait for a replay by watching the tail's completion word (its last
         // store) rather than for the stream's completion signal; the stream is
         // polled too, so a failure ends the wait with its error
         bool wait_timed_out = false;
         auto wait_tail = [&]() -> hipError_t {
             const double t_wait = now_s();
-            for (unsigned spin = 1; *done != ta.ticket; spin++) {
+            for (unsigned spin = 1; *done != ticket; spin++) {
                 if ((spin & 255) == 0) {
                     if ((spin & 0xfffff) == 0 && now_s() - t_wait > host_wait_limit_s()) {
                         wait_timed_out = true;
                         return hipErrorNotReady;
                     }
                     const hipError_t q = hipStreamQuery(c->stream);
-                    if (q == hipSuccess && *done == ta.ticket)
+                    if (q == hipSuccess && *done == ticket)
                         break;
                     if (q != hipErrorNotReady) {
                         const hipError_t e = hipStreamSynchronize(c->stream);
                         if (e != hipSuccess)
                             return e;
-                        return *done == ta.ticket ? hipSuccess : hipErrorUnknown;
+                        return *done == ticket ? hipSuccess : hipErrorUnknown;
                     }
                 }
             }
@@ -1657,9 +1670,12 @@ int search_impl(pastar_ctx *c, const SearchCfg &cfg, pastar_result *res)
                     gi++;
             }
             hipGraphExec_t ex = run_exec(gi);
+            expect_tail();
             hipError_t e = ex ? hipGraphLaunch(ex, c->stream) : enqueue_steps(kStepRuns[gi]);
-            if (e == hipSuccess)
+            if (e == hipSuccess && !ex)
                 e = enqueue_tail();
+            if (e != hipSuccess)
+                c->tail_ticket--;  // (no tail was enqueued: the device's count stays where it was)
             if (e == hipSuccess)
                 e = wait_tail();
             if (e != hipSuccess) {
