@@ -3098,10 +3098,10 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
     walk_chain<N, KW>(Pp, table, cap_mask, start, max, local_only, masks, last_key, info);
 }
 
-// The backtrace walk many steps per memory round trip (one shard, 1-word
-// keys, 2 <= N <= 6; same result as walk_kernel with local_only = 0).  Most
-// columns of an alignment hold no gap: their parent mask steps back in every
-// sequence at once.  One wave: lane j fetches the first probe line of the node
+// The backtrace walk many steps per memory round trip (one shard; 1-word
+// keys of 2..6 sequences, 2-word keys of 7 or 8; same result as walk_kernel
+// with local_only = 0).  Most columns of an alignment hold no gap: their
+// parent mask steps back in every sequence at once.  One wave: lane j fetches the first probe line of the node
 // j such steps behind the current one (lane 0: the node itself).  The records
 // that came back tell in one ballot how far the path keeps to that diagonal;
 // the first record with another mask, if it is at hand, is the round's last
@@ -3111,31 +3111,50 @@ __global__ void walk_kernel(const DevProblem *__restrict__ Pp, const uint64_t *_
 // lane's mask goes out in one store.  A node missing from its first line (a
 // displaced key, rare at the table's load) is looked up along its probe
 // chain when it is the round's first, and ends the round before it otherwise.
-template <int N>
+// (fixed N: 1-word keys of 2..6 sequences, 2-word keys of 7 or 8)
+__host__ __device__ constexpr bool walk_ahead_ok(int n, int kw)
+{
+    return (kw == 1 && n >= 2 && n <= 6) || (kw == 2 && n >= 7 && n <= 8);
+}
+
+template <int N, int KW>
 __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
                                             uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
                                             int32_t *__restrict__ masks, uint64_t *__restrict__ last_key,
                                             int *__restrict__ info, unsigned long long *dbg = nullptr)
 {
-    static_assert(N >= 2 && N <= 6, "fixed N, 1-word keys");
+    static_assert(N >= 2 && KW >= 1 && KW <= 2, "fixed N; 1-word keys by the line, 2-word keys by the slot");
 #ifdef PASTAR_PHASE_TIMERS
     const unsigned long long w_t0 = device_clock();
     unsigned long long w_t1 = 0, w_t2 = 0, w_rounds = 0, w_fetch = 0;
 #endif
-    constexpr int SW = slot_words<1>();
-    constexpr int LS = line_slots<1>();
+    constexpr int SW = slot_words<KW>();
+    constexpr int LS = KW == 1 ? line_slots<1>() : 1;  // slots compared: a 1-word key's probe line, a 2-word key's first slot
     constexpr uint32_t kFull = (1u << N) - 1;  // the mask of a step back in every sequence at once
     const DevProblem &Pg = *Pp;
-    const KConst<N, 1> P = load_kconst<N, 1>(Pg);
+    const KConst<N, KW> P = load_kconst<N, KW>(Pg);
     const int lane = lane_id();
     // one step back in every sequence, and this lane's `lane` of them
-    uint64_t diag = 0;
+    // (a sequence's position is a field of one key word: no borrow crosses words)
+    uint64_t diag[KW], dec[KW], origin[KW], key[KW];
 #pragma unroll
-    for (int i = 0; i < N; i++)
-        diag += 1ull << P.kshift[i];
-    const uint64_t dec = diag * (uint64_t)lane;
-    const uint64_t origin = Pg.origin_key[0];
-    uint64_t key = start[0];  // uniform
+    for (int k = 0; k < KW; k++) {
+        diag[k] = 0;
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (KW == 1 || P.kword[i] == k)
+                diag[k] += 1ull << P.kshift[i];
+        dec[k] = diag[k] * (uint64_t)lane;
+        origin[k] = Pg.origin_key[k];
+        key[k] = start[k];  // uniform
+    }
+    auto same = [](const uint64_t (&x)[KW], const uint64_t (&y)[KW]) {
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            eq &= x[k] == y[k];
+        return eq;
+    };
     int steps = 0, status = 0;
     while (status == 0) {
 #ifdef PASTAR_PHASE_TIMERS
@@ -3146,7 +3165,7 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
         w_rounds++;
         const unsigned long long w_r0 = device_clock();
 #endif
-        if (key == origin) {
+        if (same(key, origin)) {
             status = 1;
             break;
         }
@@ -3155,39 +3174,49 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
             break;
         }
         int pos[N];
-        const uint64_t kk[1] = {key};
-        decode_key<N, 1>(P, N, kk, pos);
+        decode_key<N, KW>(P, N, key, pos);
         bool valid = true;  // the node `lane` steps down the diagonal exists
 #pragma unroll
         for (int i = 0; i < N; i++)
             if (pos[i] < lane)
                 valid = false;
-        const uint64_t ck = key - dec;  // lane 0: the node itself
+        uint64_t ck[KW];  // lane 0: the node itself
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            ck[k] = key[k] - dec[k];
         uint64_t best = ~0ull;
         bool found = false;
         if (valid) {
-            const uint64_t ckk[1] = {ck};
-            const uint64_t *line = table + probe_start<1>(ckk, cap_mask) * SW;
+            const uint64_t *line = table + probe_start<KW>(ck, cap_mask) * SW;
             typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-            u64x2 v[LS];
+            if constexpr (KW == 1) {
+                u64x2 v[LS];
 #pragma unroll
-            for (int t = 0; t < LS; t++)
-                v[t] = *reinterpret_cast<const u64x2 *>(line + t * SW);  // key, best
+                for (int t = 0; t < LS; t++)
+                    v[t] = *reinterpret_cast<const u64x2 *>(line + t * SW);  // key, best
 #pragma unroll
-            for (int t = 0; t < LS; t++)
-                if (!found && v[t].x == ck) {
-                    best = v[t].y;
+                for (int t = 0; t < LS; t++)
+                    if (!found && v[t].x == ck[0]) {
+                        best = v[t].y;
+                        found = true;
+                    }
+            } else {
+                const u64x2 kv = *reinterpret_cast<const u64x2 *>(line);  // key words
+                const uint64_t bv = line[KW];
+                if (kv.x == ck[0] && kv.y == ck[KW - 1]) {
+                    best = bv;
                     found = true;
                 }
+            }
         }
-        if (!(__ballot(found) & 1ull)) {  // (uniform; the rare path)
-            const int64_t s = lookup<1>(table, cap_mask, kk);
+        if (!(__ballot(found) & 1ull)) {  // (uniform; the rare path for 1-word keys, one node in a few for 2-word keys)
+            const int64_t s = lookup<KW>(table, cap_mask, key);
             if (s < 0) {
                 status = -1;
                 break;
             }
             if (lane == 0) {
-                best = table[(uint64_t)s * SW + 1];
+                best = table[(uint64_t)s * SW + KW];
                 found = true;
             }
         }
@@ -3198,13 +3227,16 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
         const uint32_t m = (uint32_t)best;  // the parent mask of this lane's node
         const uint64_t hit = __ballot(found);
         // (the origin's record carries the full mask too: it has no parent)
-        const uint64_t full = __ballot(found && m == kFull && ck != origin);
+        const uint64_t full = __ballot(found && m == kFull && !same(ck, origin));
         // (uniform from here) the run of full steps from the node on; it ends
         // at the origin at the latest
         const int run = full == ~0ull ? 64 : __builtin_ctzll(~full);
         int count = run;
-        uint64_t next = key - diag * (uint64_t)run;
-        if (next != origin && run < 64 && ((hit >> run) & 1ull)) {
+        uint64_t next[KW];
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            next[k] = key[k] - diag[k] * (uint64_t)run;
+        if (!same(next, origin) && run < 64 && ((hit >> run) & 1ull)) {
             // the record that ends the run is at hand: the round's last step
             const uint32_t ml = (uint32_t)bcast_lane((int)m, run);
             if (ml == 0 || ml > kFull) {
@@ -3214,8 +3246,12 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
             count++;
 #pragma unroll
             for (int i = 0; i < N; i++)
-                if ((ml >> i) & 1)
-                    next -= 1ull << P.kshift[i];
+                if ((ml >> i) & 1) {
+#pragma unroll
+                    for (int k = 0; k < KW; k++)
+                        if (KW == 1 || P.kword[i] == k)
+                            next[k] -= 1ull << P.kshift[i];
+                }
         }
         if (steps + count > max) {
             status = 2;
@@ -3224,10 +3260,14 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
         if (lane < count)
             masks[steps + lane] = (int32_t)m;
         steps += count;
-        key = next;
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            key[k] = next[k];
     }
     if (lane == 0) {
-        last_key[0] = key;
+#pragma unroll
+        for (int k = 0; k < KW; k++)
+            last_key[k] = key[k];
         info[0] = steps;
         info[1] = status;
 #ifdef PASTAR_PHASE_TIMERS
@@ -3242,7 +3282,7 @@ __device__ __forceinline__ void walk2_chain(const DevProblem *__restrict__ Pp, c
     }
 }
 
-template <int N>
+template <int N, int KW>
 __global__ __launch_bounds__(64) void walk2_kernel(const DevProblem *__restrict__ Pp, const uint64_t *__restrict__ table,
                                                    uint64_t cap_mask, const uint64_t *__restrict__ start, int max,
                                                    int32_t *__restrict__ masks, uint64_t *__restrict__ last_key,
@@ -3250,7 +3290,7 @@ __global__ __launch_bounds__(64) void walk2_kernel(const DevProblem *__restrict_
 {
     if (gate && *(volatile const int *)gate != 1)  // see queue_census_kernel
         return;
-    walk2_chain<N>(Pp, table, cap_mask, start, max, masks, last_key, info);
+    walk2_chain<N, KW>(Pp, table, cap_mask, start, max, masks, last_key, info);
 }
 
 // The end of a one-shard graph replay in one launch (in place of the census,
@@ -3321,13 +3361,14 @@ __global__ __launch_bounds__(kBlock) void tail_kernel(TailArgs t)
 #endif
     if (blockIdx.x == 0) {
         if (threadIdx.x < 64) {
-            constexpr bool kTwo = KW == 1 && N >= 2 && N <= 6;
+            constexpr bool kTwo = walk_ahead_ok(N, KW);
             if constexpr (kTwo)
 #ifdef PASTAR_PHASE_TIMERS
-                walk2_chain<kTwo ? N : 2>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key, t.info,
-                                          t.h_census + 5);
+                walk2_chain<kTwo ? N : 2, kTwo ? KW : 1>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key,
+                                                         t.info, t.h_census + 5);
 #else
-                walk2_chain<kTwo ? N : 2>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key, t.info);
+                walk2_chain<kTwo ? N : 2, kTwo ? KW : 1>(t.P, t.table, t.cap_mask, t.goal_key, t.max, t.masks, t.last_key,
+                                                         t.info);
 #endif
             else if (threadIdx.x == 0)
                 walk_chain<N, KW>(t.P, t.table, t.cap_mask, t.goal_key, t.max, 0, t.masks, t.last_key, t.info);

@@ -634,9 +634,9 @@ struct Impl {
     static void walk(hipStream_t s, const DevProblem *P, const uint64_t *t, uint64_t cm, const uint64_t *start, int max,
                      int local, int32_t *masks, uint64_t *last, int *info, const int *gate)
     {
-        if constexpr (KW == 1 && N >= 2 && N <= 6) {
+        if constexpr (walk_ahead_ok(N, KW)) {
             if (!local) {
-                hipLaunchKernelGGL((walk2_kernel<N>), dim3(1), dim3(64), 0, s, P, t, cm, start, max, masks, last, info,
+                hipLaunchKernelGGL((walk2_kernel<N, KW>), dim3(1), dim3(64), 0, s, P, t, cm, start, max, masks, last, info,
                                    gate);
                 return;
             }
